@@ -1,0 +1,292 @@
+/*
+ * ccoracle.c -- TEST INFRASTRUCTURE ONLY (see ccoracle.h).
+ *
+ * CPU restatement of the reference's Viterbi hot path and its producers/consumer. Each function
+ * cites the reference file:line it restates (paths relative to the reference repository root).
+ * Compiled with gcc -O2 and no -march flags so, like the reference build (CMakeLists.txt:5), no
+ * FMA contraction can change the fp32/fp64 channel arithmetic.
+ */
+#include "ccoracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- rand() / gengauss() */
+
+/* glibc srandom_r/random_r, TYPE_3 (degree 31, separation 3). The reference seeds with
+ * srand(time(NULL)) (AWGN-channel/main.c:147) and draws with rand(); golden harnesses use srand(seed). */
+void cco_srand(cco_rng* g, uint32_t seed) {
+    int32_t word = (int32_t)(seed == 0 ? 1u : seed);
+    g->s[0] = (uint32_t)word;
+    for (int i = 1; i < 31; ++i) {
+        /* 16807 * word mod (2^31 - 1), Schrage's method exactly as glibc evaluates it */
+        int32_t hi = word / 127773;
+        int32_t lo = word % 127773;
+        word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        g->s[i] = (uint32_t)word;
+    }
+    g->f = 3;
+    g->r = 0;
+    for (int i = 0; i < 310; ++i) (void)cco_rand(g);
+    g->R = 0.0;
+    g->T = 0.0;
+    g->phase = 0;
+}
+
+int32_t cco_rand(cco_rng* g) {
+    g->s[g->f] += g->s[g->r];
+    int32_t out = (int32_t)(g->s[g->f] >> 1);
+    g->f = (g->f + 1) % 31;
+    g->r = (g->r + 1) % 31;
+    return out;
+}
+
+/* common/gaussian.c:18-38: Box-Muller, cos half first, sin half cached for the next call. */
+double cco_gengauss(cco_rng* g) {
+    const double two_pi = 2.0 * 3.14159265358979323846;
+    if (g->phase == 0) {
+        double u1, u2;
+        do {
+            u1 = (double)cco_rand(g) / 2147483647.0;
+            u2 = (double)cco_rand(g) / 2147483647.0;
+        } while (u1 == 0.0);
+        g->R = sqrt(-2.0 * log(u1));
+        g->T = two_pi * u2;
+        g->phase = 1;
+        return g->R * cos(g->T);
+    }
+    g->phase = 0;
+    return g->R * sin(g->T);
+}
+
+/* ---------------------------------------------------------------- trellis */
+
+static int parity64(uint64_t v) {
+    return __builtin_popcountll(v) & 1;
+}
+
+/* AWGN-channel/viterbi-decoder.c:50-57 (and encoder.c:93-100): generator bit of (sr & poly). */
+int cco_gen_bit(uint64_t v, int gen_mode) {
+    int p = parity64(v);
+    if (gen_mode == CCO_GEN_REF_X86) {
+        /* after the xor-fold, bit 4 of the shift count is the parity of v's bits 4,12,...,60;
+         * when it is set the 5-bit-masked shift exceeds 15 and the result is 0. */
+        p &= !parity64(v & 0x1010101010101010ull);
+    }
+    return p;
+}
+
+/* AWGN-channel/viterbi-decoder.c:45-63: shift register = state << (64-K) | input << 63; the
+ * expected symbol packs polynomial 0 into its most significant bit. */
+int cco_expected_symbol(const cco_code* c, uint32_t state, int input) {
+    uint64_t sr = ((uint64_t)state << (64 - c->K)) | ((uint64_t)(input & 1) << 63);
+    int e = 0;
+    for (int k = 0; k < c->n; ++k) e = (e << 1) | cco_gen_bit(sr & c->poly[k], c->gen_mode);
+    return e;
+}
+
+void cco_trellis(const cco_code* c, uint8_t* exp_sym) {
+    uint32_t S = 1u << (c->K - 1);
+    for (uint32_t s = 0; s < S; ++s)
+        for (int i = 0; i < 2; ++i) exp_sym[2 * s + i] = (uint8_t)cco_expected_symbol(c, s, i);
+}
+
+size_t cco_steps(const cco_code* c) { return (size_t)c->blen + (size_t)c->K - 1; }
+size_t cco_info_bytes(const cco_code* c) { return ((size_t)c->blen + 7) / 8; }
+size_t cco_out_bytes(const cco_code* c) { return (cco_steps(c) + 7) / 8; }
+
+/* ---------------------------------------------------------------- producers */
+
+/* common/encoder.c:84-119: info bits MSB-first into bit 63 of a right-shifting register; K-1 zero
+ * tail bits appended (encoder.c:112-115); one n-bit symbol per step, P0 in the MSB. */
+void cco_encode_block(const cco_code* c, const uint8_t* info, uint8_t* syms) {
+    size_t T = cco_steps(c);
+    uint64_t sr = 0;
+    for (size_t t = 0; t < T; ++t) {
+        uint64_t bit = 0;
+        if (t < (size_t)c->blen) bit = (info[t / 8] >> (7 - t % 8)) & 1u;
+        sr = (sr >> 1) | (bit << 63);
+        int e = 0;
+        for (int k = 0; k < c->n; ++k) e = (e << 1) | cco_gen_bit(sr & c->poly[k], c->gen_mode);
+        syms[t] = (uint8_t)e;
+    }
+}
+
+/* common/constellations.c:6-28: unit-power Gray constellations (values as stored there). */
+void cco_constellation(int n, float* pts) {
+    static const float c1[] = {0.707107f, 0.707107f, -0.707107f, -0.707107f};
+    static const float c2[] = {0.707107f, 0.707107f, 0.707107f, -0.707107f,
+                               -0.707107f, 0.707107f, -0.707107f, -0.707107f};
+    static const float c3[] = {0.408248f, 0.408248f, 0.408248f, 1.224745f,
+                               -0.408248f, 0.408248f, -1.224745f, 0.408248f,
+                               0.408248f, -0.408248f, 1.224745f, -0.408248f,
+                               -0.408248f, -0.408248f, -0.408248f, -1.224745f};
+    const float* src = n == 1 ? c1 : n == 2 ? c2 : c3;
+    memcpy(pts, src, sizeof(float) * 2u * (1u << n));
+}
+
+/* common/demapper.c:43-45 (ndist) and :61-70 (normalised squared distances, fp32). */
+void cco_demap(int n, float x, float y, float* out) {
+    float pts[16];
+    cco_constellation(n, pts);
+    float ddx = pts[0] - pts[2];
+    float ddy = pts[1] - pts[3];
+    float ndist = (ddx * ddx) + (ddy * ddy);
+    for (int k = 0; k < (1 << n); ++k) {
+        float dx = x - pts[2 * k];
+        float dy = y - pts[2 * k + 1];
+        out[k] = ((dx * dx) + (dy * dy)) / ndist;
+    }
+}
+
+/* AWGN-channel/main.c:212-229 (info bytes by rand()%256), :93-106 (noise added per I/Q sample in
+ * double, stored back to float), common/mapper.c:54-71, common/demapper.c:61-85. */
+void cco_awgn_blocks(const cco_code* c, uint32_t seed, float scaling, size_t nblocks, uint8_t* info,
+                     float* rx) {
+    cco_rng g;
+    cco_srand(&g, seed);
+    size_t T = cco_steps(c), IB = cco_info_bytes(c), NS = (size_t)1 << c->n;
+    float pts[16];
+    cco_constellation(c->n, pts);
+    uint8_t syms[520];
+    for (size_t b = 0; b < nblocks; ++b) {
+        uint8_t* ib = info + b * IB;
+        for (size_t j = 0; j < IB; ++j) ib[j] = (uint8_t)(cco_rand(&g) % 256);
+        cco_encode_block(c, ib, syms);
+        for (size_t t = 0; t < T; ++t) {
+            float x = pts[2 * syms[t]], y = pts[2 * syms[t] + 1];
+            x = (float)((double)x + (double)scaling * cco_gengauss(&g));
+            y = (float)((double)y + (double)scaling * cco_gengauss(&g));
+            cco_demap(c->n, x, y, rx + (b * T + t) * NS);
+        }
+    }
+}
+
+/* binary-symmetric-channel/main.c:57-72 (per-bit flips with rand()%1000000 < p) and :159-172. */
+void cco_bsc_blocks(const cco_code* c, uint32_t seed, int32_t p_ppm, size_t nblocks, uint8_t* info,
+                    uint8_t* syms) {
+    cco_rng g;
+    cco_srand(&g, seed);
+    size_t T = cco_steps(c), IB = cco_info_bytes(c);
+    for (size_t b = 0; b < nblocks; ++b) {
+        uint8_t* ib = info + b * IB;
+        for (size_t j = 0; j < IB; ++j) ib[j] = (uint8_t)(cco_rand(&g) % 256);
+        uint8_t* sb = syms + b * T;
+        cco_encode_block(c, ib, sb);
+        for (size_t t = 0; t < T; ++t)
+            for (int k = 0; k < c->n; ++k)
+                if ((cco_rand(&g) % 1000000) < p_ppm) sb[t] ^= (uint8_t)(1u << k);
+    }
+}
+
+/* ---------------------------------------------------------------- decoders */
+
+/* AWGN-channel/viterbi-decoder.c:108-141 (ACS: ascending s, inputs 0 then 1, strict <, +inf init
+ * :109-112, :212-218) and :71-90 (traceback from the lowest-index argmin, tail bits included,
+ * MSB-first). The uint8_t argmin counter (:74) is widened so K >= 9 terminates. */
+void cco_viterbi_soft(const cco_code* c, const float* rx, size_t nblocks, uint8_t* out) {
+    uint32_t S = 1u << (c->K - 1);
+    size_t T = cco_steps(c), OB = cco_out_bytes(c), NS = (size_t)1 << c->n;
+    uint8_t* exp_sym = (uint8_t*)malloc(2 * S);
+    float* M = (float*)malloc(sizeof(float) * S);
+    float* N = (float*)malloc(sizeof(float) * S);
+    uint16_t* prev = (uint16_t*)malloc(sizeof(uint16_t) * S * T);
+    uint8_t* inp = (uint8_t*)malloc(S * T);
+    cco_trellis(c, exp_sym);
+    memset(prev, 0, sizeof(uint16_t) * S * T);
+    memset(inp, 0, S * T);
+    for (size_t b = 0; b < nblocks; ++b) {
+        for (uint32_t s = 0; s < S; ++s) M[s] = s ? INFINITY : 0.0f;
+        for (size_t t = 0; t < T; ++t) {
+            const float* r = rx + (b * T + t) * NS;
+            for (uint32_t s = 0; s < S; ++s) N[s] = INFINITY;
+            for (uint32_t s = 0; s < S; ++s) {
+                for (int i = 0; i < 2; ++i) {
+                    uint32_t ns = (s >> 1) | ((uint32_t)i << (c->K - 2));
+                    float m = M[s] + r[exp_sym[2 * s + i]];
+                    if (m < N[ns]) {
+                        N[ns] = m;
+                        prev[t * S + ns] = (uint16_t)s;
+                        inp[t * S + ns] = (uint8_t)i;
+                    }
+                }
+            }
+            memcpy(M, N, sizeof(float) * S);
+        }
+        uint32_t st = 0;
+        float best = INFINITY;
+        for (uint32_t s = 0; s < S; ++s)
+            if (M[s] < best) { best = M[s]; st = s; }
+        uint8_t* ob = out + b * OB;
+        memset(ob, 0, OB);
+        for (size_t t = T; t-- > 0;) {
+            ob[t / 8] |= (uint8_t)(inp[t * S + st] << (7 - t % 8));
+            st = prev[t * S + st];
+        }
+    }
+    free(exp_sym); free(M); free(N); free(prev); free(inp);
+}
+
+/* binary-symmetric-channel/viterbi-decoder.c:114-150 (uint16 metrics saturated at 0xFF00,
+ * Hamming branch metric :68-72) and :75-96 (traceback; returns the minimum as the path metric). */
+void cco_viterbi_hard(const cco_code* c, const uint8_t* syms, size_t nblocks, uint8_t* out,
+                      int32_t* path_metric) {
+    uint32_t S = 1u << (c->K - 1);
+    size_t T = cco_steps(c), OB = cco_out_bytes(c);
+    uint8_t mask = (uint8_t)((1u << c->n) - 1u);
+    uint8_t* exp_sym = (uint8_t*)malloc(2 * S);
+    uint16_t* M = (uint16_t*)malloc(sizeof(uint16_t) * S);
+    uint16_t* N = (uint16_t*)malloc(sizeof(uint16_t) * S);
+    uint16_t* prev = (uint16_t*)malloc(sizeof(uint16_t) * S * T);
+    uint8_t* inp = (uint8_t*)malloc(S * T);
+    cco_trellis(c, exp_sym);
+    memset(prev, 0, sizeof(uint16_t) * S * T);
+    memset(inp, 0, S * T);
+    for (size_t b = 0; b < nblocks; ++b) {
+        for (uint32_t s = 0; s < S; ++s) M[s] = s ? 0xFF00 : 0;
+        for (size_t t = 0; t < T; ++t) {
+            uint8_t rs = syms[b * T + t] & mask;   /* decoder_input masks (viterbi-decoder.c:235-237) */
+            for (uint32_t s = 0; s < S; ++s) N[s] = 0xFF00;
+            for (uint32_t s = 0; s < S; ++s) {
+                for (int i = 0; i < 2; ++i) {
+                    uint32_t ns = (s >> 1) | ((uint32_t)i << (c->K - 2));
+                    uint32_t m = (uint32_t)M[s] + (uint32_t)__builtin_popcount(exp_sym[2 * s + i] ^ rs);
+                    if (m > 0xFF00) m = 0xFF00;
+                    if (m < N[ns]) {
+                        N[ns] = (uint16_t)m;
+                        prev[t * S + ns] = (uint16_t)s;
+                        inp[t * S + ns] = (uint8_t)i;
+                    }
+                }
+            }
+            memcpy(M, N, sizeof(uint16_t) * S);
+        }
+        uint32_t st = 0;
+        uint16_t best = 0xFF00;
+        for (uint32_t s = 0; s < S; ++s)
+            if (M[s] < best) { best = M[s]; st = s; }
+        uint8_t* ob = out + b * OB;
+        memset(ob, 0, OB);
+        for (size_t t = T; t-- > 0;) {
+            ob[t / 8] |= (uint8_t)(inp[t * S + st] << (7 - t % 8));
+            st = prev[t * S + st];
+        }
+        if (path_metric) path_metric[b] = (int32_t)best;
+    }
+    free(exp_sym); free(M); free(N); free(prev); free(inp);
+}
+
+/* AWGN-channel/main.c:129-141: compare the first blen bits, MSB-first. */
+uint64_t cco_count_errors(const cco_code* c, const uint8_t* info, const uint8_t* out, size_t nblocks) {
+    size_t IB = cco_info_bytes(c), OB = cco_out_bytes(c);
+    uint64_t errors = 0;
+    for (size_t b = 0; b < nblocks; ++b)
+        for (int i = 0; i < c->blen; ++i) {
+            int a = (info[b * IB + i / 8] >> (7 - i % 8)) & 1;
+            int d = (out[b * OB + i / 8] >> (7 - i % 8)) & 1;
+            errors += (uint64_t)(a != d);
+        }
+    return errors;
+}

@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures in tests/golden/ from the UNMODIFIED reference.
+
+Runs only where /root/reference exists (the build container): `make -C oracle ref` compiles the
+reference sources in place into oracle/_ref/ref_harness_{awgn,bsc} (driver logic: oracle/ref_harness.c),
+and this script runs them with fixed seeds and packs what crossed the decoder boundary into one .npz
+per case (plain arrays, loaded with allow_pickle=False). The GPU box never runs this script.
+
+    python tests/golden/make_golden.py
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_DIR = os.path.join(REPO, "oracle", "_ref")
+
+# AWGN-channel/main.c:157-161 (stored there as float).
+SCALING = {0: "0.707106781186548", 2: "0.561674881261479", 4: "0.446154216921401",
+           6: "0.354392891541971", 8: "0.281504279937367"}
+
+K7 = "2:7:{blen}:F200000000000000:B600000000000000"      # (171,133)_8
+K8 = "2:8:{blen}:F900000000000000:A700000000000000"      # (371,247)_8
+# Longest block the reference encoder supports: its uint8_t output counter (common/encoder.c:15-16)
+# limits T = blen + K - 1 to 255, so blen <= 249 at K = 7.
+
+# (name, channel, code spec, seed, nblocks, channel parameter)
+CASES = [
+    ("bsc_cb0_p25000", "bsc", "cb:0", 101, 250, "25000"),
+    ("bsc_cb0_p100000", "bsc", "cb:0", 102, 250, "100000"),
+    ("bsc_cb0_p300000", "bsc", "cb:0", 103, 250, "300000"),
+    ("bsc_cb1_p50000", "bsc", "cb:1", 104, 100, "50000"),
+    ("bsc_cb2_p50000", "bsc", "cb:2", 105, 100, "50000"),
+    ("bsc_cb3_p50000", "bsc", "cb:3", 106, 100, "50000"),
+    ("bsc_cb5_p50000", "bsc", "cb:5", 107, 100, "50000"),
+    ("bsc_k7_p50000", "bsc", K7.format(blen=40), 108, 200, "50000"),
+    ("bsc_k7_p150000", "bsc", K7.format(blen=40), 109, 200, "150000"),
+    ("bsc_k8_blen200_p20000", "bsc", K8.format(blen=200), 110, 20, "20000"),
+    ("awgn_cb0_0dB", "awgn", "cb:0", 201, 200, SCALING[0]),
+    ("awgn_cb0_4dB", "awgn", "cb:0", 202, 200, SCALING[4]),
+    ("awgn_cb0_8dB", "awgn", "cb:0", 203, 200, SCALING[8]),
+    ("awgn_cb1_2dB", "awgn", "cb:1", 204, 100, SCALING[2]),
+    ("awgn_cb2_2dB", "awgn", "cb:2", 205, 100, SCALING[2]),
+    ("awgn_cb3_2dB", "awgn", "cb:3", 206, 200, SCALING[2]),
+    ("awgn_cb3_4dB", "awgn", "cb:3", 207, 200, SCALING[4]),
+    ("awgn_cb5_2dB", "awgn", "cb:5", 208, 100, SCALING[2]),
+    ("awgn_k7_2dB", "awgn", K7.format(blen=40), 209, 100, SCALING[2]),
+    ("awgn_k7_4dB", "awgn", K7.format(blen=40), 210, 100, SCALING[4]),
+    ("awgn_k8_blen200_2dB", "awgn", K8.format(blen=200), 211, 20, SCALING[2]),
+    ("awgn_k7_blen249_4dB", "awgn", K7.format(blen=249), 212, 10, SCALING[4]),
+    ("awgn_k3_blen1_2dB", "awgn", "2:3:1:A000000000000000:6000000000000000", 213, 50, SCALING[2]),
+    ("awgn_k3_blen7_2dB", "awgn", "2:3:7:A000000000000000:6000000000000000", 214, 50, SCALING[2]),
+    ("awgn_k2_2dB", "awgn", "2:2:40:C000000000000000:8000000000000000", 215, 50, SCALING[2]),
+    ("awgn_n1k3_4dB", "awgn", "1:3:40:E000000000000000", 216, 50, SCALING[4]),
+]
+
+
+def run_case(name, channel, spec, seed, nblocks, param, tmp):
+    exe = os.path.join(REF_DIR, f"ref_harness_{channel}")
+    prefix = os.path.join(tmp, name)
+    subprocess.run([exe, prefix, str(seed), str(nblocks), param, spec], check=True, timeout=120)
+    meta = {}
+    with open(prefix + ".meta") as f:
+        for line in f:
+            k, v = line.split()
+            meta[k] = v
+    n, K, blen = int(meta["n"]), int(meta["K"]), int(meta["blen"])
+    polys = np.array([int(meta[f"poly{k}"], 16) for k in range(n)], dtype=np.uint64)
+    T = blen + K - 1
+    IB, OB = (blen + 7) // 8, (T + 7) // 8
+    arrays = {
+        "info": np.fromfile(prefix + ".info", dtype=np.uint8).reshape(nblocks, IB),
+        "out": np.fromfile(prefix + ".out", dtype=np.uint8).reshape(nblocks, OB),
+        "n": np.int32(n), "K": np.int32(K), "blen": np.int32(blen), "polys": polys,
+        "seed": np.uint32(seed), "errors": np.uint64(int(meta["errors"])),
+    }
+    if channel == "awgn":
+        arrays["rx"] = np.fromfile(prefix + ".rx", dtype=np.float32).reshape(nblocks, T, 1 << n)
+        arrays["scaling"] = np.float32(float(param))
+    else:
+        arrays["rx"] = np.fromfile(prefix + ".rx", dtype=np.uint8).reshape(nblocks, T)
+        arrays["p_ppm"] = np.int32(int(param))
+        arrays["path_metric"] = np.fromfile(prefix + ".pm", dtype=np.int32).reshape(nblocks)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
+    return {"name": name, "channel": channel, "spec": spec, "seed": seed, "nblocks": nblocks,
+            "param": param, "errors": int(meta["errors"])}
+
+
+def main():
+    if not os.path.isdir("/root/reference"):
+        sys.exit("make_golden.py needs /root/reference (build container only)")
+    subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
+    manifest = []
+    with tempfile.TemporaryDirectory() as tmp:
+        for case in CASES:
+            manifest.append(run_case(*case, tmp))
+            print(manifest[-1])
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
