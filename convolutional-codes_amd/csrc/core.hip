@@ -1,0 +1,298 @@
+// core.hip -- libccv_core.so: plans, kernel selection, launches and the ccv_* C ABI (include/ccv.h).
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "acs_generic.hpp"
+#include "ccv.h"
+#include "reg_codes.hpp"
+#include "trellis.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return -1;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail("%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                      __FILE__, __LINE__);                             \
+  } while (0)
+
+struct DeviceBuffer {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int grow(size_t need, hipStream_t sync_stream) {
+    if (need <= bytes) return 0;
+    if (ptr) {
+      HIP_TRY(hipStreamSynchronize(sync_stream));
+      HIP_TRY(hipFree(ptr));
+      ptr = nullptr;
+      bytes = 0;
+    }
+    HIP_TRY(hipMalloc(&ptr, need));
+    bytes = need;
+    return 0;
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+};
+
+}  // namespace
+
+struct ccv_plan {
+  ccv_plan_desc d{};
+  uint64_t polys[ccv::kMaxN] = {};
+  std::vector<uint8_t> exp;          // [S][2]
+  int reg_index = -1;                // kRegCodes index, or -1 for the generic kernel
+  int generic_spt = 1, generic_threads = 64, generic_chunk = 1;
+  size_t generic_lds = 0;
+  uint8_t* d_exp = nullptr;          // device copy of exp (generic kernel)
+  DeviceBuffer dec;                  // register-kernel decision scratch
+  DeviceBuffer host_in, host_out, host_pm;   // staging for ccv_decode_host
+  hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
+};
+
+namespace {
+
+int find_reg_kernel(const ccv_plan& p) {
+  using namespace ccv;
+  const int S = 1 << (p.d.K - 1);
+  std::vector<uint8_t> tab(2 * (size_t)S);
+  for (size_t i = 0; i < kNumRegCodes; ++i) {
+    const CodeSpec& c = kRegCodes[i];
+    if (c.n != p.d.n || c.K != p.d.K) continue;
+    build_trellis(c.n, c.K, c.poly, c.gen, tab.data());
+    if (tab == p.exp) return (int)i;
+  }
+  return -1;
+}
+
+template <int SPT, bool HARD>
+hipError_t launch_generic_t(const ccv::GenericArgs& a, const ccv_plan& p, size_t nblocks,
+                            hipStream_t s) {
+  const void* fn = reinterpret_cast<const void*>(&ccv::viterbi_generic<SPT, HARD>);
+  if (p.generic_lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)p.generic_lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((ccv::viterbi_generic<SPT, HARD>), dim3((unsigned)nblocks),
+                     dim3(p.generic_threads), p.generic_lds, s, a);
+  return hipGetLastError();
+}
+
+template <bool HARD>
+hipError_t launch_generic(const ccv::GenericArgs& a, const ccv_plan& p, size_t nblocks,
+                          hipStream_t s) {
+  switch (p.generic_spt) {
+    case 1: return launch_generic_t<1, HARD>(a, p, nblocks, s);
+    case 2: return launch_generic_t<2, HARD>(a, p, nblocks, s);
+    case 4: return launch_generic_t<4, HARD>(a, p, nblocks, s);
+    default: return launch_generic_t<8, HARD>(a, p, nblocks, s);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ccv_last_error(void) { return g_last_error.c_str(); }
+
+int ccv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const uint64_t* polys,
+                    int gen_mode, unsigned flags) {
+  if (!out) return fail("ccv_plan_create: null output pointer");
+  *out = nullptr;
+  if (channel != CCV_SOFT && channel != CCV_HARD) return fail("bad channel %d", channel);
+  if (n < 1 || n > ccv::kMaxN) return fail("n=%d unsupported (1..%d)", n, ccv::kMaxN);
+  if (K < 2 || K > ccv::kMaxK) return fail("K=%d unsupported (2..%d)", K, ccv::kMaxK);
+  if (blen < 1 || blen > 255) return fail("blen=%d unsupported (1..255)", blen);
+  if (!polys) return fail("null polynomials");
+  if (gen_mode != CCV_GEN_REF_X86 && gen_mode != CCV_GEN_TRUE_PARITY)
+    return fail("bad generator mode %d", gen_mode);
+
+  ccv_plan* p = new ccv_plan();
+  p->d.channel = channel;
+  p->d.n = n;
+  p->d.K = K;
+  p->d.blen = blen;
+  p->d.gen_mode = gen_mode;
+  p->d.steps = blen + K - 1;
+  p->d.states = 1 << (K - 1);
+  p->d.info_bytes = (blen + 7) / 8;
+  p->d.out_bytes = (p->d.steps + 7) / 8;
+  p->d.in_step_bytes = channel == CCV_SOFT ? (int)sizeof(float) << n : 1;
+  memcpy(p->polys, polys, sizeof(uint64_t) * (size_t)n);
+  p->exp.resize(2 * (size_t)p->d.states);
+  ccv::build_trellis(n, K, p->polys, gen_mode, p->exp.data());
+
+  hipError_t e = hipGetDevice(&p->d.device);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    delete p;
+    return fail("no HIP device: %s", hipGetErrorString(e));
+  }
+  p->reg_index = (flags & CCV_FLAG_GENERIC) ? -1 : find_reg_kernel(*p);
+  if (p->reg_index >= 0) {
+    p->d.kernel = CCV_KERNEL_REGISTER;
+    p->d.decision_word_bytes = p->d.states > 32 ? 8 : 4;
+  } else {
+    const int S = p->d.states;
+    p->d.kernel = CCV_KERNEL_GENERIC;
+    p->generic_spt = S <= ccv::kGenericMaxThreads ? 1 : S / ccv::kGenericMaxThreads;
+    p->generic_threads = S <= 64 ? 64 : (S <= ccv::kGenericMaxThreads ? S : ccv::kGenericMaxThreads);
+    const int NS = 1 << n;
+    p->generic_chunk = 4096 / NS < 1 ? 1 : 4096 / NS;
+    if (p->generic_chunk > p->d.steps) p->generic_chunk = p->d.steps;
+    p->generic_lds = ccv::generic_lds_bytes(n, K, p->d.steps, p->generic_chunk, channel == CCV_HARD);
+    if (p->generic_lds > 160 * 1024) {
+      delete p;
+      return fail("code needs %zu B of LDS per block", p->generic_lds);
+    }
+    if (hipMalloc(&p->d_exp, p->exp.size()) != hipSuccess ||
+        hipMemcpy(p->d_exp, p->exp.data(), p->exp.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipGetLastError();
+      if (p->d_exp) (void)hipFree(p->d_exp);
+      delete p;
+      return fail("device table upload failed");
+    }
+  }
+  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    if (p->d_exp) (void)hipFree(p->d_exp);
+    delete p;
+    return fail("hipStreamCreate failed");
+  }
+  *out = p;
+  return 0;
+}
+
+void ccv_plan_destroy(ccv_plan* p) {
+  if (!p) return;
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  p->dec.release();
+  p->host_in.release();
+  p->host_out.release();
+  p->host_pm.release();
+  if (p->d_exp) (void)hipFree(p->d_exp);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+}
+
+int ccv_plan_describe(const ccv_plan* p, ccv_plan_desc* desc) {
+  if (!p || !desc) return fail("null argument");
+  *desc = p->d;
+  return 0;
+}
+
+int ccv_plan_trellis(const ccv_plan* p, uint8_t* exp) {
+  if (!p || !exp) return fail("null argument");
+  memcpy(exp, p->exp.data(), p->exp.size());
+  return 0;
+}
+
+int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {
+  if (!p) return fail("null plan");
+  if (p->reg_index < 0) return 0;
+  return p->dec.grow(max_blocks * (size_t)p->d.steps * (size_t)p->d.decision_word_bytes, p->stream);
+}
+
+int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_out,
+                      int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
+                      void* d_decisions, void* stream_v) {
+  if (!p) return fail("null plan");
+  if (nblocks == 0) return 0;
+  if (!d_in || !d_out) return fail("null device buffer");
+  if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+  const bool hard = p->d.channel == CCV_HARD;
+  if (p->reg_index >= 0) {
+    ccv::RegArgs a{};
+    a.in = d_in;
+    a.T = p->d.steps;
+    a.nblocks = (int)nblocks;
+    a.blen = p->d.blen;
+    a.out = d_out;
+    a.path_metric = hard ? d_path_metric : nullptr;
+    a.info = d_info;
+    a.err = d_info ? d_errors : nullptr;
+    if (d_decisions) {
+      a.dec = d_decisions;
+    } else {
+      if (p->dec.grow(nblocks * (size_t)p->d.steps * (size_t)p->d.decision_word_bytes, stream))
+        return -1;
+      a.dec = p->dec.ptr;
+    }
+    const int grid = (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads);
+    const ccv::RegLaunchFn* fns = hard ? ccv::hard_reg_launchers() : ccv::soft_reg_launchers();
+    HIP_TRY(fns[p->reg_index](a, grid, stream));
+  } else {
+    if (d_decisions) return fail("decision export needs the register kernel");
+    ccv::GenericArgs a{};
+    a.in = d_in;
+    a.exp = p->d_exp;
+    a.n = p->d.n;
+    a.K = p->d.K;
+    a.T = p->d.steps;
+    a.blen = p->d.blen;
+    a.nblocks = (int)nblocks;
+    a.chunk = p->generic_chunk;
+    a.out = d_out;
+    a.path_metric = hard ? d_path_metric : nullptr;
+    a.info = d_info;
+    a.err = d_info ? d_errors : nullptr;
+    HIP_TRY(hard ? launch_generic<true>(a, *p, nblocks, stream)
+                 : launch_generic<false>(a, *p, nblocks, stream));
+  }
+  return 0;
+}
+
+int ccv_decode_host(ccv_plan* p, const void* in, size_t nblocks, uint8_t* out, int32_t* path_metric) {
+  if (!p) return fail("null plan");
+  if (nblocks == 0) return 0;
+  if (!in || !out) return fail("null host buffer");
+  const size_t in_bytes = nblocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes;
+  const size_t out_bytes = nblocks * (size_t)p->d.out_bytes;
+  const bool want_pm = p->d.channel == CCV_HARD && path_metric;
+  if (p->host_in.grow(in_bytes, p->stream) || p->host_out.grow(out_bytes, p->stream)) return -1;
+  if (want_pm && p->host_pm.grow(nblocks * sizeof(int32_t), p->stream)) return -1;
+  HIP_TRY(hipMemcpyAsync(p->host_in.ptr, in, in_bytes, hipMemcpyHostToDevice, p->stream));
+  if (ccv_decode_device(p, p->host_in.ptr, nblocks, static_cast<uint8_t*>(p->host_out.ptr),
+                        want_pm ? static_cast<int32_t*>(p->host_pm.ptr) : nullptr, nullptr, nullptr,
+                        nullptr, p->stream))
+    return -1;
+  HIP_TRY(hipMemcpyAsync(out, p->host_out.ptr, out_bytes, hipMemcpyDeviceToHost, p->stream));
+  if (want_pm)
+    HIP_TRY(hipMemcpyAsync(path_metric, p->host_pm.ptr, nblocks * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, p->stream));
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  return 0;
+}
+
+}  // extern "C"

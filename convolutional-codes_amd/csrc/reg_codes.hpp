@@ -1,0 +1,41 @@
+// reg_codes.hpp -- codes that get an ahead-of-time register-trellis kernel (acs_reg.hpp).
+//
+// The plan matches a code by its expected-symbol TABLE, not by its polynomials, so two descriptions
+// with the same trellis (e.g. codebook code 0 in either generator mode) share one kernel. Codes
+// not listed here run on the table-driven kernel (acs_generic.hpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "acs_reg.hpp"
+#include "trellis.hpp"
+
+namespace ccv {
+
+#define CCV_CODE2(K, P0, P1, GEN) \
+  CodeSpec { 2, K, {P0##ull, P1##ull, 0, 0, 0, 0, 0, 0}, GEN }
+#define CCV_CODE3(K, P0, P1, P2, GEN) \
+  CodeSpec { 3, K, {P0##ull, P1##ull, P2##ull, 0, 0, 0, 0, 0}, GEN }
+
+inline constexpr CodeSpec kRegCodes[] = {
+    // common/codebook.c:14-54, codes 0-3 and 5 (code 4 is the K=32 WSPR code: no Viterbi)
+    CCV_CODE2(3, 0xA000000000000000, 0x6000000000000000, GEN_REF_X86),
+    CCV_CODE2(4, 0xB000000000000000, 0xE000000000000000, GEN_REF_X86),
+    CCV_CODE2(4, 0xB000000000000000, 0xE000000000000000, GEN_TRUE_PARITY),
+    CCV_CODE2(5, 0xA800000000000000, 0xF000000000000000, GEN_REF_X86),
+    CCV_CODE2(5, 0xA800000000000000, 0xF000000000000000, GEN_TRUE_PARITY),
+    CCV_CODE2(6, 0xB400000000000000, 0xE800000000000000, GEN_REF_X86),
+    CCV_CODE2(6, 0xB400000000000000, 0xE800000000000000, GEN_TRUE_PARITY),
+    CCV_CODE3(3, 0xA000000000000000, 0xC000000000000000, 0x2000000000000000, GEN_REF_X86),
+    // K=7 (171,133)_8, the benchmark code (BASELINE.json configs 2 and 4)
+    CCV_CODE2(7, 0xF200000000000000, 0xB600000000000000, GEN_REF_X86),
+    CCV_CODE2(7, 0xF200000000000000, 0xB600000000000000, GEN_TRUE_PARITY),
+};
+inline constexpr size_t kNumRegCodes = sizeof(kRegCodes) / sizeof(kRegCodes[0]);
+
+using RegLaunchFn = hipError_t (*)(const RegArgs&, int grid, hipStream_t stream);
+const RegLaunchFn* soft_reg_launchers();   // [kNumRegCodes], reg_soft.hip
+const RegLaunchFn* hard_reg_launchers();   // [kNumRegCodes], reg_hard.hip
+
+}  // namespace ccv

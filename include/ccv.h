@@ -1,0 +1,91 @@
+/*
+ * ccv.h -- C ABI of the MI355X (gfx950) Viterbi decoder core, libccv_core.so.
+ *
+ * This is the batched, device-level API underneath the reference-compatible decoder_* shims
+ * (include/decoder_awgn.h, include/decoder_bsc.h). It replaces, for whole batches of independent
+ * zero-tail-terminated trellis blocks, the per-step work the reference does in
+ *   receive_symbol()/get_transition_metric()  AWGN-channel/viterbi-decoder.c:38-69,108-141
+ *                                             binary-symmetric-channel/viterbi-decoder.c:38-73,114-150
+ *   traceback()                               AWGN-channel/viterbi-decoder.c:71-90
+ *                                             binary-symmetric-channel/viterbi-decoder.c:75-96
+ * and the bit-error count of the drivers' decoded callbacks (AWGN-channel/main.c:118-144,
+ * binary-symmetric-channel/main.c:74-98).
+ *
+ * Data layouts (identical to what the reference decoder consumes and emits, block after block):
+ *   soft input  float   [nblocks][T][2^n]   demapper output per trellis step (common/demapper.c:66-70)
+ *   hard input  uint8_t [nblocks][T]        received symbol per step, low n bits used
+ *   output      uint8_t [nblocks][OB]       MSB-first decoded bits, OB = ceil(T/8), tail bits included
+ *   info        uint8_t [nblocks][IB]       transmitted info bits (optional), IB = ceil(blen/8)
+ * with T = blen + K - 1.  All functions return 0 on success and -1 on failure (ccv_last_error()).
+ * Not thread-safe per plan: use one plan per thread (as the reference decoder handle).
+ */
+#ifndef CCV_H
+#define CCV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCV_SOFT 0            /* AWGN soft decision: float branch metrics per expected symbol   */
+#define CCV_HARD 1            /* BSC hard decision: Hamming branch metric, uint16-saturating    */
+
+#define CCV_GEN_REF_X86 0     /* generator bit as the reference computes it on x86 (default)    */
+#define CCV_GEN_TRUE_PARITY 1 /* textbook parity generator                                      */
+
+#define CCV_FLAG_GENERIC 1u   /* force the table-driven kernel even if a specialised one exists */
+
+#define CCV_KERNEL_REGISTER 1 /* code-specialised register-trellis kernel                       */
+#define CCV_KERNEL_GENERIC 2  /* table-driven LDS kernel                                        */
+
+typedef struct ccv_plan ccv_plan;
+
+typedef struct {
+    int channel, n, K, blen, gen_mode;
+    int steps;           /* T  */
+    int states;          /* S = 2^(K-1) */
+    int info_bytes;      /* IB */
+    int out_bytes;       /* OB */
+    int in_step_bytes;   /* 4 * 2^n (soft) or 1 (hard) */
+    int kernel;          /* CCV_KERNEL_* */
+    int decision_word_bytes; /* register kernel: bytes of one step's decisions per block */
+    int device;
+} ccv_plan_desc;
+
+/* A plan binds a code to the device that is current on the calling thread.
+ * n in [1,8], K in [2,12], blen in [1,255]; polys[0..n-1] MSB-aligned (code.h:13). */
+int ccv_plan_create(ccv_plan** plan, int channel, int n, int K, int blen, const uint64_t* polys,
+                    int gen_mode, unsigned flags);
+void ccv_plan_destroy(ccv_plan* plan);
+int ccv_plan_describe(const ccv_plan* plan, ccv_plan_desc* desc);
+
+/* Expected-symbol table of the plan's trellis: exp[2*s + i], S*2 bytes. */
+int ccv_plan_trellis(const ccv_plan* plan, uint8_t* exp);
+
+/* Grow the plan's device scratch so decodes of up to max_blocks blocks allocate nothing. */
+int ccv_plan_reserve(ccv_plan* plan, size_t max_blocks);
+
+/* Asynchronous decode of nblocks device-resident blocks on `stream` (a hipStream_t; NULL = the
+ * legacy default stream).  d_path_metric (hard only), d_info + d_errors (error counting: adds the
+ * batch's bit errors over the first blen bits to *d_errors) and d_decisions (register kernel only:
+ * [T][nblocks] words of ccv_plan_desc.decision_word_bytes, bit s = survivor of state s came from
+ * the odd predecessor) may be NULL. */
+int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t* d_out,
+                      int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
+                      void* d_decisions, void* stream);
+
+/* Synchronous convenience: host buffers in and out (staged through plan-owned device buffers). */
+int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out,
+                    int32_t* path_metric);
+
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int ccv_device_count(void);
+
+const char* ccv_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,103 @@
+"""The oracle (oracle/ccoracle.c) pinned against the reference's own outputs (tests/golden/*.npz,
+generated from the unmodified reference by tests/golden/make_golden.py) and against glibc."""
+import ctypes
+import ctypes.util
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from conftest import golden_manifest
+
+CASES = golden_manifest()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_matches_reference_fixture(case):
+    g = O.load_golden(case["name"])
+    c = O.golden_code(g)
+    nb = g["info"].shape[0]
+    # producers: the reference driver's rand() stream from srand(seed), bit for bit
+    if case["channel"] == "awgn":
+        info, rx = O.awgn_blocks(c, int(g["seed"]), float(g["scaling"]), nb)
+        assert np.array_equal(rx.view(np.uint32), g["rx"].view(np.uint32))
+        out = O.viterbi_soft(c, g["rx"])
+    else:
+        info, syms = O.bsc_blocks(c, int(g["seed"]), int(g["p_ppm"]), nb)
+        assert np.array_equal(syms, g["rx"])
+        out, pm = O.viterbi_hard(c, g["rx"])
+        assert np.array_equal(pm, g["path_metric"])
+    assert np.array_equal(info, g["info"])
+    # decoder: the reference's whole output buffer (tail bits included)
+    assert np.array_equal(out, g["out"])
+    # consumer: error count of the reference driver
+    assert O.count_errors(c, g["info"], out) == int(g["errors"]) == case["errors"]
+
+
+def test_rand_restatement_matches_glibc():
+    libc = ctypes.CDLL(ctypes.util.find_library("c"))
+    for seed in (1, 2, 12345, 0xC0DE, 2**31 - 1):
+        libc.srand(seed)
+        expect = [libc.rand() for _ in range(2000)]
+        g = O.CcoRng()
+        O.lib().cco_srand(ctypes.byref(g), seed)
+        got = [O.lib().cco_rand(ctypes.byref(g)) for _ in range(2000)]
+        assert got == expect
+
+
+def test_rand_known_answer():
+    g = O.CcoRng()
+    O.lib().cco_srand(ctypes.byref(g), 1)
+    assert [O.lib().cco_rand(ctypes.byref(g)) for _ in range(3)] == [1804289383, 846930886, 1681692777]
+
+
+def test_generator_idiom_vs_true_parity_tables():
+    """codes 0 and 5 are unaffected by the x86 shift idiom;
+    the K=7 (171,133) table differs in 48 of 128 entries, code 3 (K=6) in 16 of 64."""
+    def diff(n, K, polys):
+        a = O.trellis(O.code(n, K, 40, polys, O.GEN_REF_X86))
+        b = O.trellis(O.code(n, K, 40, polys, O.GEN_TRUE_PARITY))
+        return int(np.count_nonzero(a != b))
+    assert diff(2, 3, [0xA000000000000000, 0x6000000000000000]) == 0
+    assert diff(3, 3, [0xA000000000000000, 0xC000000000000000, 0x2000000000000000]) == 0
+    assert diff(2, 7, [0xF200000000000000, 0xB600000000000000]) == 48
+    assert diff(2, 6, [0xB400000000000000, 0xE800000000000000]) == 16
+
+
+def test_gen_bit_idiom_definition():
+    rng = np.random.default_rng(7)
+    for v in rng.integers(0, 2**63, size=2000, dtype=np.uint64).tolist() + [0, 2**64 - 1, 1 << 60]:
+        v = int(v)
+        fold = v ^ (v >> 32)
+        fold ^= fold >> 16
+        fold ^= fold >> 8
+        fold = (fold & ~0xF) | ((fold ^ (fold >> 4)) & 0xF)   # val ^= (val >> 4) & 0x0F
+        shift = fold & 31                                        # x86 shl/sar masks the count to 5 bits
+        expect = (0x6996 >> shift) & 1
+        assert O.lib().cco_gen_bit(v, O.GEN_REF_X86) == expect
+        assert O.lib().cco_gen_bit(v, O.GEN_TRUE_PARITY) == bin(v).count("1") % 2
+
+
+def test_encoder_impulse_response_true_parity():
+    """A single 1 followed by zeros emits the generator taps (true-parity mode)."""
+    c = O.code(2, 7, 40, [0xF200000000000000, 0xB600000000000000], O.GEN_TRUE_PARITY)
+    info = np.zeros(5, np.uint8)
+    info[0] = 0x80
+    syms = O.encode_block(c, info)
+    taps0 = [(0xF2 >> (7 - j)) & 1 for j in range(7)]
+    taps1 = [(0xB6 >> (7 - j)) & 1 for j in range(7)]
+    assert [int(s) >> 1 for s in syms[:7]] == taps0
+    assert [int(s) & 1 for s in syms[:7]] == taps1
+    assert not syms[7:].any()
+
+
+def test_oracle_statistical_ber_code0_4dB():
+    """Published BER 0.05668375 at 4 dB (results/awgn_channel.m:15) within a 99.9% interval."""
+    c = O.code(2, 3, 40, [0xA000000000000000, 0x6000000000000000])
+    nb = 5000
+    info, rx = O.awgn_blocks(c, 4242, np.float32(0.446154216921401), nb)
+    errs = O.count_errors(c, info, O.viterbi_soft(c, rx))
+    bits = nb * 40
+    p = 0.05668375
+    # bit errors of a Viterbi decoder come in bursts: allow a generous 5-sigma binomial band
+    assert abs(errs / bits - p) < 5 * np.sqrt(p * (1 - p) / bits) * 3
