@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--code", default="k7", help="k7, k9, code0..code5 (suffix :true = true parity)")
     ap.add_argument("--frames", type=int, default=16, help="1 M-bit frames per GPU per step")
     ap.add_argument("--ebn0", type=float, default=4.0)
+    ap.add_argument("--layout", choices=("block", "step"), default="block",
+                    help="input layout in HBM: block-major [nb][T][4] as the reference decoder consumes "
+                         "it, or step-major [T][nb][4] (CCV_FLAG_STEP_MAJOR)")
     ap.add_argument("--seed", type=int, default=0xC0DE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline work budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -119,6 +122,7 @@ def main():
     import torch.distributed as dist
 
     from ccviterbi import SOFT, Plan, channel as ch, named_code
+    from ccviterbi.decoder import FLAG_STEP_MAJOR
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -134,11 +138,12 @@ def main():
     # this rank's frames: blocks [rank*nb, (rank+1)*nb) of the Philox stream
     info, rx = ch.awgn_blocks(code, nb, ch.noise_scaling(args.ebn0), args.seed, first_block=rank * nb,
                               threads=cpu_threads())
-    d_rx = torch.from_numpy(rx).to("cuda")
+    host_in = rx if args.layout == "block" else np.ascontiguousarray(rx.transpose(1, 0, 2))
+    d_rx = torch.from_numpy(host_in).to("cuda")
     d_info = torch.from_numpy(info).to("cuda")
     d_out = torch.empty((nb, code.out_bytes), dtype=torch.uint8, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
-    plan = Plan(code, SOFT)
+    plan = Plan(code, SOFT, FLAG_STEP_MAJOR if args.layout == "step" else 0)
     plan.reserve(nb)
     stream = torch.cuda.current_stream()
 
@@ -177,7 +182,7 @@ def main():
         bpb = algorithmic_bytes_per_bit(code)
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-        workload_key = f"{args.code}:frames{args.frames}"
+        workload_key = f"{args.code}:frames{args.frames}:{args.layout}"
         traffic = load_pmc_traffic(workload_key)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -206,6 +211,8 @@ def main():
                 "ebn0_db": args.ebn0,
                 "parallelism": f"dp{world} (frames sharded, counters all-reduced once)",
                 "kernel": plan.kernel,
+                "input_layout": "block-major [nb][T][2^n] (reference)" if args.layout == "block"
+                                else "step-major [T][nb][2^n]",
             },
             "ber": {"ebn0_db": args.ebn0, "errors": errors, "bits": bits_per_step * args.steps,
                     "ber": errors / (bits_per_step * args.steps)},

@@ -17,6 +17,7 @@ from .code import GEN_REF_X86, HARD, SOFT, Code
 
 KERNEL_REGISTER, KERNEL_GENERIC = 1, 2
 FLAG_GENERIC = 1
+FLAG_STEP_MAJOR = 2
 
 
 class DecoderError(RuntimeError):

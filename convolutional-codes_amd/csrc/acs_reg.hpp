@@ -12,8 +12,9 @@
 // predecessor is visited first and is kept on ties. No permutation between lanes is ever needed,
 // so the only per-state cost is 2 adds + min + sub + shift-in.
 //
-// Decisions (S bits per step) go to a [T][nblocks] array of 32/64-bit words, one coalesced store per
-// wave per step; after the last step the same lane finds the lowest-index minimum and walks its own
+// Decisions (S bits per step) go to a [T][dec_stride] array of 32/64-bit words (dec_stride = nblocks
+// rounded up to a whole wave, so every lane stores unconditionally), one coalesced store per wave per
+// step; after the last step the same lane finds the lowest-index minimum and walks its own
 // decisions back (reference :71-90), writing the reference's MSB-first output buffer (tail bits
 // included) and, optionally, counting bit errors against the transmitted info bits
 // (consumer AWGN-channel/main.c:118-144) with one atomic per wave.
@@ -100,16 +101,19 @@ __device__ __forceinline__ DecWord<(1 << (C.K - 1))> acs_step(MT (&M)[1 << (C.K 
 }
 
 struct RegArgs {
-  const void* in;          // soft: float [nb][T][2^n]; hard: uint8 [nb][T]
+  const void* in;          // soft: float [nb][T][2^n] (or [T][nb][2^n], step-major); hard: uint8 [nb][T]
   int T;
   int nblocks;
   int blen;
+  int dec_stride;          // blocks per decision row: nblocks rounded up to kRegThreads
   uint8_t* out;            // [nb][OB]
   int32_t* path_metric;    // hard only, may be null
-  void* dec;               // [T][nb] DecWord
+  void* dec;               // [T][dec_stride] DecWord
   const uint8_t* info;     // optional [nb][IB] transmitted info bytes (error counting)
   unsigned long long* err; // optional error accumulator
 };
+
+constexpr int kRegThreads = 64;   // one wave per workgroup: spreads small batches over more CUs
 
 // Lowest-index minimum (reference traceback :72-79, strict < from the sentinel).
 template <int S, typename MT>
@@ -130,14 +134,14 @@ template <int K>
 __device__ __forceinline__ uint32_t traceback(const RegArgs& a, int b, uint32_t st) {
   constexpr int S = 1 << (K - 1);
   using DW = DecWord<S>;
-  const DW* dec = reinterpret_cast<const DW*>(a.dec);
-  const int T = a.T, nb = a.nblocks, OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+  const DW* dec = reinterpret_cast<const DW*>(a.dec) + b;
+  const int T = a.T, OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+  const size_t stride = (size_t)a.dec_stride;
   uint32_t errors = 0;
   for (int lo = (T - 1) & ~7; lo >= 0; lo -= 8) {
     DW d[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (lo + k < T) d[k] = dec[(size_t)(lo + k) * nb + b];
+    for (int k = 0; k < 8; ++k) d[k] = dec[(size_t)(lo + k < T ? lo + k : T - 1) * stride];
     uint32_t acc = 0;
 #pragma unroll
     for (int k = 7; k >= 0; --k) {
@@ -165,43 +169,149 @@ __device__ __forceinline__ void accumulate_errors(const RegArgs& a, uint32_t err
   if ((threadIdx.x & 63) == 0 && errors) atomicAdd(a.err, (unsigned long long)errors);
 }
 
-constexpr int kRegThreads = 64;   // one wave per workgroup: spreads small batches over more CUs
-constexpr int kPrefetch = 4;      // trellis steps of input kept in flight per lane
+// Steps [t_begin, T) with PF steps of input in flight. The main loop is straight-line (no bounds
+// checks, every load and store unconditional) so the compiler can wait for each load with a counted
+// vmcnt instead of draining the memory pipe (stores included) every iteration.
+template <int PF, class In, class Load, class Step>
+__device__ __forceinline__ void pipelined_steps(int t_begin, int T, Load&& load, Step&& step) {
+  In ring[PF];
+#pragma unroll
+  for (int k = 0; k < PF; ++k) ring[k] = load(t_begin + k < T ? t_begin + k : T - 1);
+  int t = t_begin;
+  for (; t + 2 * PF <= T; t += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      In cur = ring[u];
+      ring[u] = load(t + u + PF);
+      step(cur, t + u);
+    }
+  }
+  for (; t < T; t += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (t + u < T) {
+        In cur = ring[u];
+        if (t + u + PF < T) ring[u] = load(t + u + PF);
+        step(cur, t + u);
+      }
+    }
+  }
+}
 
-template <CodeSpec C>
+// How a lane gets its block's per-step input.
+enum SoftLoad : int {
+  kLoadPerStep = 0,    // block-major input, each lane loads its own step (64 cache lines per load)
+  kLoadStepMajor = 2,  // step-major input [T][nblocks][2^n]: one 1 KiB coalesced load per step
+  kLoadLdsDma = 3,     // block-major input, the wave stages PF steps of its 64 blocks in LDS with
+                       // global_load_lds (LDS-DMA, no VGPR staging); each lane then reads its own
+                       // chunk into registers and the next chunk's DMA runs under the ACS
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Ablation switches for timing studies (tools/kbench.hip); production kernels use 0.
+enum : int { kAblateDecStore = 1, kAblateTraceback = 2 };
+
+// Soft-decision register-trellis kernel. MODE selects the input path (SoftLoad); PF is the input
+// prefetch depth in steps (per-step modes) or the steps staged per LDS round (kLoadLdsDma).
+template <CodeSpec C, int MODE, int PF, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) void viterbi_soft_reg(RegArgs a) {
   constexpr int S = 1 << (C.K - 1);
   constexpr int NS = 1 << C.n;
   using DW = DecWord<S>;
-  const int b = blockIdx.x * kRegThreads + threadIdx.x;
-  uint32_t errors = 0;
-  if (b < a.nblocks) {
-    const int T = a.T, nb = a.nblocks;
-    const float* p = reinterpret_cast<const float*>(a.in) + (size_t)b * T * NS;
-    DW* dec = reinterpret_cast<DW*>(a.dec) + b;
-    float M[S];
+  const int lane = threadIdx.x;
+  const int block0 = blockIdx.x * kRegThreads;
+  const int b = block0 + lane;
+  const int T = a.T, nb = a.nblocks;
+  DW* dec = reinterpret_cast<DW*>(a.dec) + b;   // padded rows: every lane owns a column
+  const size_t dstride = (size_t)a.dec_stride;
+  float M[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) M[s] = s ? __builtin_inff() : 0.0f;   // viterbi-decoder.c:212-218
-    SoftStep<NS> ring[kPrefetch];
+  for (int s = 0; s < S; ++s) M[s] = s ? __builtin_inff() : 0.0f;   // viterbi-decoder.c:212-218
+  auto step = [&](const SoftStep<NS>& in, int t) {
+    DW d = acs_step<C, false, float>(M, in.v);
+    if constexpr ((ABLATE & kAblateDecStore) != 0) asm volatile("" ::"v"(d));
+    else dec[(size_t)t * dstride] = d;
+  };
+
+  if constexpr (MODE == kLoadLdsDma) {
+    static_assert(NS >= 4, "LDS-DMA staging needs 16-byte trellis steps");
+    constexpr int SB = NS * 4;                 // bytes per trellis step
+    constexpr int UPR = PF * SB / 16;          // 16-byte units per block per chunk (= DMAs per chunk)
+    static_assert(UPR == 4 || UPR == 8 || UPR == 16, "chunk must be 64, 128 or 256 bytes per block");
+    constexpr int ROWB = UPR * 16;
+    constexpr int GRP = 16 / UPR;
+    // LDS image [block r][slot j]: slot j of row r holds 16-byte unit j ^ sw(r) of block r's chunk.
+    // The DMA writes lane-linearly, so the swizzle is applied to the per-lane SOURCE address; with
+    // sw(r) = (r / GRP) % UPR every ds_read_b128 lane group (MI355X_MICROARCH.md, LDS) touches 16
+    // distinct 16-byte bank groups: conflict-free.
+    __shared__ __attribute__((aligned(16))) unsigned char lds[kRegThreads * ROWB];
+    const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
+    const size_t block_bytes = (size_t)T * SB;
+    auto issue_chunk = [&](int t0) {
 #pragma unroll
-    for (int k = 0; k < kPrefetch; ++k)
-      if (k < T) ring[k] = load_soft_step<NS>(p + k * NS);
-    for (int t = 0; t < T; t += kPrefetch) {
+      for (int k = 0; k < UPR; ++k) {
+        const int unit = k * kRegThreads + lane;
+        const int r = unit / UPR, j = unit % UPR;
+        const int su = j ^ ((r / GRP) % UPR);
+        const int gb = block0 + r < nb ? block0 + r : nb - 1;
+        size_t off = (size_t)t0 * SB + (size_t)su * 16;
+        off = off < block_bytes ? off : block_bytes - 16;   // past the block: clamped, never read
+        __builtin_amdgcn_global_load_lds(in + (size_t)gb * block_bytes + off,
+                                         (lds_ptr_t)(lds + k * kRegThreads * 16), 16, 0, 0);
+      }
+    };
+    const int sw = (lane / GRP) % UPR;
+    const unsigned char* row = lds + lane * ROWB;
+    issue_chunk(0);
+    for (int t0 = 0; t0 < T; t0 += PF) {
+      float4 chunk[UPR];
 #pragma unroll
-      for (int u = 0; u < kPrefetch; ++u) {
-        if (t + u < T) {
-          SoftStep<NS> cur = ring[u];
-          if (t + u + kPrefetch < T) ring[u] = load_soft_step<NS>(p + (t + u + kPrefetch) * NS);
-          dec[(size_t)(t + u) * nb] = acs_step<C, false, float>(M, cur.v);
+      for (int x = 0; x < UPR; ++x) chunk[x] = *reinterpret_cast<const float4*>(row + ((x ^ sw) * 16));
+      if (t0 + PF < T) {
+        // the chunk is in registers once these reads return; only then may the DMA overwrite it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue_chunk(t0 + PF);                  // lands while this chunk is decoded
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if (t0 + u < T) {
+          SoftStep<NS> cur;
+#pragma unroll
+          for (int q = 0; q < NS / 4; ++q) {
+            const float4 v = chunk[u * (NS / 4) + q];
+            cur.v[4 * q] = v.x; cur.v[4 * q + 1] = v.y; cur.v[4 * q + 2] = v.z; cur.v[4 * q + 3] = v.w;
+          }
+          step(cur, t0 + u);
         }
       }
     }
+  } else {
+    // per-lane step loads: block-major (64 distinct lines per load) or step-major (coalesced)
+    const int bc = b < nb ? b : nb - 1;   // lanes past the batch replay a valid block
+    const float* p = reinterpret_cast<const float*>(a.in) +
+                     (MODE == kLoadStepMajor ? (size_t)bc * NS : (size_t)bc * T * NS);
+    const size_t stride = MODE == kLoadStepMajor ? (size_t)nb * NS : (size_t)NS;
+    pipelined_steps<PF, SoftStep<NS>>(0, T, [&](int t) { return load_soft_step<NS>(p + t * stride); }, step);
+  }
+  uint32_t errors = 0;
+  if (b < nb) {
     float best;
     uint32_t st = (uint32_t)argmin_state<S, float>(M, __builtin_inff(), best);
-    errors = traceback<C.K>(a, b, st);
+    if constexpr ((ABLATE & kAblateTraceback) != 0) a.out[b] = (uint8_t)st;
+    else errors = traceback<C.K>(a, b, st);
   }
   accumulate_errors(a, errors);
 }
+
+// Production input path for block-major soft input: LDS-DMA staging in 4-step chunks where a step
+// is at least 16 bytes (n >= 2), per-lane loads otherwise (tools/kbench.hip compares the paths).
+template <int NS>
+inline constexpr int kSoftMode = NS >= 4 ? kLoadLdsDma : kLoadPerStep;
+template <int NS>
+inline constexpr int kSoftPF = NS >= 4 ? 4 : 8;
+constexpr int kSoftStepMajorPF = 4;        // prefetch depth, step-major input
+constexpr int kHardPF = 8;                 // prefetch depth, hard decision
 
 template <CodeSpec C>
 __global__ __launch_bounds__(kRegThreads) void viterbi_hard_reg(RegArgs a) {
@@ -209,42 +319,35 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_hard_reg(RegArgs a) {
   constexpr int NS = 1 << C.n;
   using DW = DecWord<S>;
   const int b = blockIdx.x * kRegThreads + threadIdx.x;
+  const int T = a.T, nb = a.nblocks;
+  const int bc = b < nb ? b : nb - 1;
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(a.in) + (size_t)bc * T;
+  DW* dec = reinterpret_cast<DW*>(a.dec) + b;
+  const size_t dstride = (size_t)a.dec_stride;
+  constexpr uint32_t kMask = NS - 1;   // decoder_input masks to n bits (viterbi-decoder.c:235-237)
+  uint32_t M[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) M[s] = s ? 0xFF00u : 0u;   // viterbi-decoder.c:225-228
+  auto branch_metrics = [](uint32_t sym, uint32_t (&BM)[NS]) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) BM[k] = __builtin_popcount((uint32_t)k ^ (sym & kMask));
+  };
+  // The first K-1 steps still have unreachable states, whose metrics saturate at 0xFF00 as in the
+  // reference; afterwards every metric is <= n*T < 0xFF00 - n and saturation is a no-op.
+  const int t0 = T < C.K - 1 ? T : C.K - 1;
+  for (int t = 0; t < t0; ++t) {
+    uint32_t BM[NS];
+    branch_metrics(p[t], BM);
+    dec[(size_t)t * dstride] = acs_step<C, true, uint32_t>(M, BM);
+  }
+  pipelined_steps<kHardPF, uint32_t>(t0, T, [&](int t) { return (uint32_t)p[t]; },
+                                     [&](uint32_t sym, int t) {
+                                       uint32_t BM[NS];
+                                       branch_metrics(sym, BM);
+                                       dec[(size_t)t * dstride] = acs_step<C, false, uint32_t>(M, BM);
+                                     });
   uint32_t errors = 0;
-  if (b < a.nblocks) {
-    const int T = a.T, nb = a.nblocks;
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(a.in) + (size_t)b * T;
-    DW* dec = reinterpret_cast<DW*>(a.dec) + b;
-    constexpr uint32_t kMask = NS - 1;   // decoder_input masks to n bits (viterbi-decoder.c:235-237)
-    uint32_t M[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) M[s] = s ? 0xFF00u : 0u;   // viterbi-decoder.c:225-228
-    // The first K-1 steps still have unreachable states, whose metrics saturate at 0xFF00 as in
-    // the reference; afterwards every metric is <= n*T < 0xFF00 - n and saturation is a no-op.
-    const int t0 = T < C.K - 1 ? T : C.K - 1;
-    for (int t = 0; t < t0; ++t) {
-      uint32_t sym = p[t] & kMask;
-      uint32_t BM[NS];
-#pragma unroll
-      for (int k = 0; k < NS; ++k) BM[k] = __builtin_popcount((uint32_t)k ^ sym);
-      dec[(size_t)t * nb] = acs_step<C, true, uint32_t>(M, BM);
-    }
-    uint32_t ring[kPrefetch];
-#pragma unroll
-    for (int k = 0; k < kPrefetch; ++k)
-      if (t0 + k < T) ring[k] = p[t0 + k];
-    for (int t = t0; t < T; t += kPrefetch) {
-#pragma unroll
-      for (int u = 0; u < kPrefetch; ++u) {
-        if (t + u < T) {
-          uint32_t sym = ring[u] & kMask;
-          if (t + u + kPrefetch < T) ring[u] = p[t + u + kPrefetch];
-          uint32_t BM[NS];
-#pragma unroll
-          for (int k = 0; k < NS; ++k) BM[k] = __builtin_popcount((uint32_t)k ^ sym);
-          dec[(size_t)(t + u) * nb] = acs_step<C, false, uint32_t>(M, BM);
-        }
-      }
-    }
+  if (b < nb) {
     uint32_t best;
     uint32_t st = (uint32_t)argmin_state<S, uint32_t>(M, 0xFF00u, best);
     if (a.path_metric) a.path_metric[b] = (int32_t)best;

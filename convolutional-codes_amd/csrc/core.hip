@@ -62,6 +62,7 @@ struct ccv_plan {
   uint64_t polys[ccv::kMaxN] = {};
   std::vector<uint8_t> exp;          // [S][2]
   int reg_index = -1;                // kRegCodes index, or -1 for the generic kernel
+  bool step_major = false;           // soft input layout [T][nblocks][2^n] (CCV_FLAG_STEP_MAJOR)
   int generic_spt = 1, generic_threads = 64, generic_chunk = 1;
   size_t generic_lds = 0;
   uint8_t* d_exp = nullptr;          // device copy of exp (generic kernel)
@@ -71,6 +72,14 @@ struct ccv_plan {
 };
 
 namespace {
+
+size_t padded_blocks(size_t nblocks) {
+  return (nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads * ccv::kRegThreads;
+}
+
+size_t decision_bytes(const ccv_plan& p, size_t nblocks) {
+  return padded_blocks(nblocks) * (size_t)p.d.steps * (size_t)p.d.decision_word_bytes;
+}
 
 int find_reg_kernel(const ccv_plan& p) {
   using namespace ccv;
@@ -158,7 +167,16 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
     delete p;
     return fail("no HIP device: %s", hipGetErrorString(e));
   }
+  p->step_major = (flags & CCV_FLAG_STEP_MAJOR) != 0;
+  if (p->step_major && channel != CCV_SOFT) {
+    delete p;
+    return fail("step-major input is a soft-decision layout");
+  }
   p->reg_index = (flags & CCV_FLAG_GENERIC) ? -1 : find_reg_kernel(*p);
+  if (p->step_major && p->reg_index < 0) {
+    delete p;
+    return fail("step-major input needs a register-trellis code");
+  }
   if (p->reg_index >= 0) {
     p->d.kernel = CCV_KERNEL_REGISTER;
     p->d.decision_word_bytes = p->d.states > 32 ? 8 : 4;
@@ -220,7 +238,7 @@ int ccv_plan_trellis(const ccv_plan* p, uint8_t* exp) {
 int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {
   if (!p) return fail("null plan");
   if (p->reg_index < 0) return 0;
-  return p->dec.grow(max_blocks * (size_t)p->d.steps * (size_t)p->d.decision_word_bytes, p->stream);
+  return p->dec.grow(decision_bytes(*p, max_blocks), p->stream);
 }
 
 int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_out,
@@ -238,6 +256,7 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     a.T = p->d.steps;
     a.nblocks = (int)nblocks;
     a.blen = p->d.blen;
+    a.dec_stride = (int)padded_blocks(nblocks);
     a.out = d_out;
     a.path_metric = hard ? d_path_metric : nullptr;
     a.info = d_info;
@@ -245,12 +264,12 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     if (d_decisions) {
       a.dec = d_decisions;
     } else {
-      if (p->dec.grow(nblocks * (size_t)p->d.steps * (size_t)p->d.decision_word_bytes, stream))
-        return -1;
+      if (p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
       a.dec = p->dec.ptr;
     }
     const int grid = (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads);
-    const ccv::RegLaunchFn* fns = hard ? ccv::hard_reg_launchers() : ccv::soft_reg_launchers();
+    const ccv::RegLaunchFn* fns =
+        hard ? ccv::hard_reg_launchers() : ccv::soft_reg_launchers(p->step_major);
     HIP_TRY(fns[p->reg_index](a, grid, stream));
   } else {
     if (d_decisions) return fail("decision export needs the register kernel");
@@ -275,6 +294,7 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
 
 int ccv_decode_host(ccv_plan* p, const void* in, size_t nblocks, uint8_t* out, int32_t* path_metric) {
   if (!p) return fail("null plan");
+  if (p->step_major) return fail("ccv_decode_host takes block-major input");
   if (nblocks == 0) return 0;
   if (!in || !out) return fail("null host buffer");
   const size_t in_bytes = nblocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes;

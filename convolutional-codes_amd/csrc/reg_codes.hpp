@@ -35,7 +35,7 @@ inline constexpr CodeSpec kRegCodes[] = {
 inline constexpr size_t kNumRegCodes = sizeof(kRegCodes) / sizeof(kRegCodes[0]);
 
 using RegLaunchFn = hipError_t (*)(const RegArgs&, int grid, hipStream_t stream);
-const RegLaunchFn* soft_reg_launchers();   // [kNumRegCodes], reg_soft.hip
+const RegLaunchFn* soft_reg_launchers(bool step_major);   // [kNumRegCodes], reg_soft.hip
 const RegLaunchFn* hard_reg_launchers();   // [kNumRegCodes], reg_hard.hip
 
 }  // namespace ccv

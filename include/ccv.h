@@ -36,6 +36,8 @@ extern "C" {
 #define CCV_GEN_TRUE_PARITY 1 /* textbook parity generator                                      */
 
 #define CCV_FLAG_GENERIC 1u   /* force the table-driven kernel even if a specialised one exists */
+#define CCV_FLAG_STEP_MAJOR 2u /* soft input is step-major float [T][nblocks][2^n] (coalesced;
+                                  register-trellis codes only; ccv_decode_device only)            */
 
 #define CCV_KERNEL_REGISTER 1 /* code-specialised register-trellis kernel                       */
 #define CCV_KERNEL_GENERIC 2  /* table-driven LDS kernel                                        */
@@ -70,8 +72,9 @@ int ccv_plan_reserve(ccv_plan* plan, size_t max_blocks);
 /* Asynchronous decode of nblocks device-resident blocks on `stream` (a hipStream_t; NULL = the
  * legacy default stream).  d_path_metric (hard only), d_info + d_errors (error counting: adds the
  * batch's bit errors over the first blen bits to *d_errors) and d_decisions (register kernel only:
- * [T][nblocks] words of ccv_plan_desc.decision_word_bytes, bit s = survivor of state s came from
- * the odd predecessor) may be NULL. */
+ * [T][P] words of ccv_plan_desc.decision_word_bytes, P = nblocks rounded up to a multiple of 64,
+ * block b in column b; bit s set = the survivor into state s came from the odd predecessor) may be
+ * NULL. */
 int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t* d_out,
                       int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
                       void* d_decisions, void* stream);

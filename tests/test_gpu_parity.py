@@ -224,7 +224,10 @@ def _device(torch, arr):
 
 
 @pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY])
-def test_full_frame_noiseless_round_trip(torch_cuda, gen):
+def test_full_frame_noiseless(torch_cuda, gen):
+    """True parity: (171,133) is a proper non-catastrophic code, so a noiseless frame decodes with
+    zero errors. The x86-idiom variant is not injective (some butterflies emit the same symbol for
+    both inputs), so even noiseless frames keep errors -- there the check is equality with the oracle."""
     torch = torch_cuda
     c = K7.with_(gen_mode=gen)
     info, rx = ch.awgn_blocks(c, FRAME, 0.0, 2024)
@@ -234,9 +237,14 @@ def test_full_frame_noiseless_round_trip(torch_cuda, gen):
     plan.decode_device(_device(torch, rx), FRAME, d_out, d_info=_device(torch, info), d_errors=d_err)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
-    assert int(d_err.item()) == 0
-    assert np.array_equal(np.unpackbits(out, axis=1)[:, :c.blen], np.unpackbits(info, axis=1)[:, :c.blen])
-    assert not np.unpackbits(out, axis=1)[:, c.blen:c.steps].any()   # zero tail decoded
+    assert int(d_err.item()) == ch.count_bit_errors(c, info, out)
+    if gen == GEN_TRUE_PARITY:
+        assert int(d_err.item()) == 0
+        bits = np.unpackbits(out, axis=1)
+        assert np.array_equal(bits[:, :c.blen], np.unpackbits(info, axis=1)[:, :c.blen])
+        assert not bits[:, c.blen:c.steps].any()   # the zero tail decodes as zeros
+    idx = np.arange(0, FRAME, 89)
+    assert np.array_equal(out[idx], O.viterbi_soft(_ocode(c), rx[idx]))
 
 
 def test_full_frame_error_count_decisions_and_determinism(torch_cuda):
@@ -247,7 +255,7 @@ def test_full_frame_error_count_decisions_and_determinism(torch_cuda):
     d_rx, d_info = _device(torch, rx), _device(torch, info)
     d_out = torch.empty((FRAME, c.out_bytes), dtype=torch.uint8, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
-    d_dec = torch.empty((c.steps, FRAME), dtype=torch.int64, device="cuda")
+    d_dec = torch.empty((c.steps, (FRAME + 63) // 64 * 64), dtype=torch.int64, device="cuda")
     plan.decode_device(d_rx, FRAME, d_out, d_info=d_info, d_errors=d_err, d_decisions=d_dec)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
@@ -292,11 +300,14 @@ def test_full_frame_bsc_k7(torch_cuda):
     ref, ref_pm = O.viterbi_hard(_ocode(K7), syms[idx])
     assert np.array_equal(d_out.cpu().numpy()[idx], ref)
     assert np.array_equal(d_pm.cpu().numpy()[idx], ref_pm)
-    # path metric = Hamming distance between the re-encoded survivor and the received symbols
+    # path metric = Hamming distance between the survivor path re-encoded from the zero state (all T
+    # decided inputs, tail decisions included: the traceback is not forced to end in state 0) and
+    # the received symbols
     out = d_out.cpu().numpy()
-    recoded = ch.encode(K7, out[:, :K7.info_bytes] & np.uint8(0xFF))
+    full = K7.with_(blen=K7.steps)                  # encode T input bits, keep the first T symbols
+    recoded = ch.encode(full, out)[:, :K7.steps]
     dist = np.unpackbits((recoded ^ syms)[..., None], axis=-1)[..., -2:].sum(axis=(1, 2))
-    assert np.array_equal(dist[idx], d_pm.cpu().numpy()[idx])
+    assert np.array_equal(dist, d_pm.cpu().numpy())
 
 
 def test_statistical_ber_code0_matches_published(torch_cuda):

@@ -1,0 +1,6 @@
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out/pmc
+rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE" "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU"; do
+  tag=$(echo $set | cut -d' ' -f1)
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $set --output-format csv -d gpurun_out/pmc/$tag -o run -- ./tools/kbench 400000 3 true/step-major4 > gpurun_out/pmc/$tag.log 2>&1 || exit $?
+done
