@@ -317,3 +317,21 @@ def test_statistical_ber_code0_matches_published(torch_cuda):
                         seed=31)
     assert abs(pts[0].ber - 0.05668375) / 0.05668375 < 0.05
     assert abs(pts[1].ber - 0.00545587) / 0.00545587 < 0.1
+
+
+@pytest.mark.parametrize("c", [K7, K7.with_(gen_mode=GEN_TRUE_PARITY), CODEBOOK[0], CODEBOOK[5]],
+                         ids=["k7", "k7_true", "code0", "code5"])
+def test_step_major_layout_matches(torch_cuda, c):
+    """CCV_FLAG_STEP_MAJOR: the same frames transposed to [T][nb][2^n] decode identically."""
+    from ccviterbi.decoder import FLAG_STEP_MAJOR
+    torch = torch_cuda
+    nb = 3001
+    info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 17)
+    d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    Plan(c, SOFT, FLAG_STEP_MAJOR).decode_device(_device(torch, rx.transpose(1, 0, 2)), nb, d_out,
+                                                  d_info=_device(torch, info), d_errors=d_err)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
+    assert int(d_err.item()) == ch.count_bit_errors(c, info, out)

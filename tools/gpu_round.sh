@@ -12,7 +12,7 @@ rc=$?; echo "smoke rc=$rc"; [ $rc -ne 0 ] && { tail -30 $OUT/smoke.log; exit $rc
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps $STEPS --warmup 3 > $OUT/bench.log 2>&1
+timeout -k 10 600 python bench.py --steps $STEPS --warmup 3 > $OUT/bench.log 2>&1 && timeout -k 10 300 python bench.py --steps $STEPS --warmup 3 --layout step --no-cpu-baseline > $OUT/bench_step.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 $OUT/bench.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
     python bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1
