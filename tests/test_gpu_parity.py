@@ -335,3 +335,30 @@ def test_step_major_layout_matches(torch_cuda, c):
     out = d_out.cpu().numpy()
     assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
     assert int(d_err.item()) == ch.count_bit_errors(c, info, out)
+
+
+DROPIN_CASES = [c for c in CASES if c["name"] in (
+    "awgn_cb0_4dB", "awgn_k7_2dB", "awgn_cb5_2dB", "awgn_k3_blen7_2dB", "bsc_cb0_p100000", "bsc_k7_p50000")]
+
+
+@pytest.mark.parametrize("case", DROPIN_CASES, ids=lambda c: c["name"])
+def test_reference_driver_with_mi355x_decoder(case, tmp_path):
+    """Drop-in check: oracle/ref_harness.c -- the reference drivers' producer chain and callback
+    logic, compiled against the reference's own headers -- linked to libccv_{awgn,bsc}.so instead of
+    the reference decoder, reproduces the reference's output files byte for byte."""
+    import os
+    import subprocess
+    from conftest import REPO
+    exe = os.path.join(REPO, "oracle", "_ref", f"ref_harness_{case['channel']}_ccv")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref drop-in harness not built (needs /root/reference at build time)")
+    g = O.load_golden(case["name"])
+    prefix = str(tmp_path / case["name"])
+    subprocess.run([exe, prefix, str(case["seed"]), str(case["nblocks"]), case["param"], case["spec"]],
+                   check=True, timeout=300)
+    out = np.fromfile(prefix + ".out", dtype=np.uint8).reshape(g["out"].shape)
+    assert np.array_equal(out, g["out"])
+    if case["channel"] == "bsc":
+        assert np.array_equal(np.fromfile(prefix + ".pm", dtype=np.int32), g["path_metric"])
+    meta = dict(line.split() for line in open(prefix + ".meta"))
+    assert int(meta["errors"]) == case["errors"]
