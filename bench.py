@@ -108,7 +108,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--code", default="k7", help="k7, k9, code0..code5 (suffix :true = true parity)")
-    ap.add_argument("--frames", type=int, default=16, help="1 M-bit frames per GPU per step")
+    ap.add_argument("--frames", type=int, default=64,
+                    help="1 M-bit frames per GPU per step (64 = 1.6 M blocks = 25,000 one-wave tiles, "
+                         "~6 waves per SIMD so the last partial round is a small fraction)")
     ap.add_argument("--ebn0", type=float, default=4.0)
     ap.add_argument("--layout", choices=("block", "step"), default="block",
                     help="input layout in HBM: block-major [nb][T][4] as the reference decoder consumes "

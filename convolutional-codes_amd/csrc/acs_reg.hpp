@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "trellis.hpp"
 
 namespace ccv {
@@ -52,7 +54,7 @@ struct SoftStep {
   float v[NS];
 };
 
-template <int NS>
+template <int NS, int NT = 0>
 __device__ __forceinline__ SoftStep<NS> load_soft_step(const float* p) {
   SoftStep<NS> r;
   if constexpr (NS == 2) {
@@ -61,7 +63,14 @@ __device__ __forceinline__ SoftStep<NS> load_soft_step(const float* p) {
   } else if constexpr (NS % 4 == 0) {
 #pragma unroll
     for (int q = 0; q < NS / 4; ++q) {
-      float4 a = reinterpret_cast<const float4*>(p)[q];
+      float4 a;
+      if constexpr (NT) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p) + q);
+        a = float4{v.x, v.y, v.z, v.w};
+      } else {
+        a = reinterpret_cast<const float4*>(p)[q];
+      }
       r.v[4 * q] = a.x; r.v[4 * q + 1] = a.y; r.v[4 * q + 2] = a.z; r.v[4 * q + 3] = a.w;
     }
   } else {
@@ -181,9 +190,11 @@ __device__ __forceinline__ void pipelined_steps(int t_begin, int T, Load&& load,
   for (; t + 2 * PF <= T; t += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
-      In cur = ring[u];
+      // consume the slot, then refill it: the load can land in the same registers, so the loop
+      // back-edge needs no copies (a copy would wait for the load and collapse the prefetch)
+      step(ring[u], t + u);
       ring[u] = load(t + u + PF);
-      step(cur, t + u);
+      __builtin_amdgcn_sched_barrier(0);   // keep each refill at its step (the scheduler sinks them)
     }
   }
   for (; t < T; t += PF) {
@@ -210,11 +221,11 @@ enum SoftLoad : int {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // Ablation switches for timing studies (tools/kbench.hip); production kernels use 0.
-enum : int { kAblateDecStore = 1, kAblateTraceback = 2 };
+enum : int { kAblateDecStore = 1, kAblateTraceback = 2, kAblateLoads = 4 };
 
 // Soft-decision register-trellis kernel. MODE selects the input path (SoftLoad); PF is the input
 // prefetch depth in steps (per-step modes) or the steps staged per LDS round (kLoadLdsDma).
-template <CodeSpec C, int MODE, int PF, int ABLATE = 0>
+template <CodeSpec C, int MODE, int PF, int ABLATE = 0, int NT = 0>
 __global__ __launch_bounds__(kRegThreads) void viterbi_soft_reg(RegArgs a) {
   constexpr int S = 1 << (C.K - 1);
   constexpr int NS = 1 << C.n;
@@ -257,8 +268,9 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_soft_reg(RegArgs a) {
         const int gb = block0 + r < nb ? block0 + r : nb - 1;
         size_t off = (size_t)t0 * SB + (size_t)su * 16;
         off = off < block_bytes ? off : block_bytes - 16;   // past the block: clamped, never read
+        // NT: the input is read exactly once -- keep it from displacing the decision scratch
         __builtin_amdgcn_global_load_lds(in + (size_t)gb * block_bytes + off,
-                                         (lds_ptr_t)(lds + k * kRegThreads * 16), 16, 0, 0);
+                                         (lds_ptr_t)(lds + k * kRegThreads * 16), 16, 0, NT ? 2 : 0);
       }
     };
     const int sw = (lane / GRP) % UPR;
@@ -292,7 +304,17 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_soft_reg(RegArgs a) {
     const float* p = reinterpret_cast<const float*>(a.in) +
                      (MODE == kLoadStepMajor ? (size_t)bc * NS : (size_t)bc * T * NS);
     const size_t stride = MODE == kLoadStepMajor ? (size_t)nb * NS : (size_t)NS;
-    pipelined_steps<PF, SoftStep<NS>>(0, T, [&](int t) { return load_soft_step<NS>(p + t * stride); }, step);
+    if constexpr ((ABLATE & kAblateLoads) != 0) {
+      for (int t = 0; t < T; ++t) {   // synthetic input from registers: VALU-only timing
+        SoftStep<NS> in;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) in.v[k] = (float)((lane + t + k) & 7);
+        step(in, t);
+      }
+    } else {
+      pipelined_steps<PF, SoftStep<NS>>(0, T, [&](int t) { return load_soft_step<NS, NT>(p + t * stride); },
+                                        step);
+    }
   }
   uint32_t errors = 0;
   if (b < nb) {
@@ -304,12 +326,13 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_soft_reg(RegArgs a) {
   accumulate_errors(a, errors);
 }
 
-// Production input path for block-major soft input: LDS-DMA staging in 4-step chunks where a step
-// is at least 16 bytes (n >= 2), per-lane loads otherwise (tools/kbench.hip compares the paths).
+// Production input path for block-major soft input: LDS-DMA staging where a step is at least 16
+// bytes (n >= 2) -- 8-step (128-byte) chunks for n = 2, 4-step chunks for n = 3 -- per-lane loads
+// otherwise (tools/kbench.hip compares the paths; profiles/r01_kbench_variants.txt).
 template <int NS>
 inline constexpr int kSoftMode = NS >= 4 ? kLoadLdsDma : kLoadPerStep;
 template <int NS>
-inline constexpr int kSoftPF = NS >= 4 ? 4 : 8;
+inline constexpr int kSoftPF = NS == 4 ? 8 : (NS >= 8 ? 4 : 8);
 constexpr int kSoftStepMajorPF = 4;        // prefetch depth, step-major input
 constexpr int kHardPF = 8;                 // prefetch depth, hard decision
 

@@ -28,9 +28,9 @@ struct Variant {
   bool step_major;
 };
 
-template <CodeSpec C, int MODE, int PF, int AB = 0>
+template <CodeSpec C, int MODE, int PF, int AB = 0, int NT = 0>
 void launch_v(const RegArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((viterbi_soft_reg<C, MODE, PF, AB>), dim3(grid), dim3(kRegThreads), 0, s, a);
+  hipLaunchKernelGGL((viterbi_soft_reg<C, MODE, PF, AB, NT>), dim3(grid), dim3(kRegThreads), 0, s, a);
 }
 
 int main(int argc, char** argv) {
@@ -69,12 +69,23 @@ int main(int argc, char** argv) {
       {"true/lds-dma8", launch_v<kK7True, kLoadLdsDma, 8>, false},
       {"true/step-major4", launch_v<kK7True, kLoadStepMajor, 4>, true},
       {"true/step-major8", launch_v<kK7True, kLoadStepMajor, 8>, true},
+      {"ref/dma4-nt", launch_v<kK7Ref, kLoadLdsDma, 4, 0, 1>, false},
+      {"ref/dma8-nt", launch_v<kK7Ref, kLoadLdsDma, 8, 0, 1>, false},
+      {"ref/sm4-nt", launch_v<kK7Ref, kLoadStepMajor, 4, 0, 1>, true},
+      {"true/dma4-nt", launch_v<kK7True, kLoadLdsDma, 4, 0, 1>, false},
+      {"true/dma8-nt", launch_v<kK7True, kLoadLdsDma, 8, 0, 1>, false},
+      {"true/sm4-nt", launch_v<kK7True, kLoadStepMajor, 4, 0, 1>, true},
       {"true/sm4-nodecst", launch_v<kK7True, kLoadStepMajor, 4, kAblateDecStore>, true},
       {"true/sm4-notb", launch_v<kK7True, kLoadStepMajor, 4, kAblateTraceback>, true},
       {"true/sm4-neither", launch_v<kK7True, kLoadStepMajor, 4, 3>, true},
       {"true/ps8-neither", launch_v<kK7True, kLoadPerStep, 8, 3>, false},
+      {"true/noload-neither", launch_v<kK7True, kLoadStepMajor, 4, 7>, true},
+      {"ref/noload-neither", launch_v<kK7Ref, kLoadStepMajor, 4, 7>, true},
+      {"true/noload", launch_v<kK7True, kLoadStepMajor, 4, 4>, true},
   };
   const int nv = sizeof(vs) / sizeof(vs[0]);
+  const char* ring_env = getenv("KB_FRAMES");   // >1: rotate over distinct input copies (> MALL)
+  (void)ring_env;
   std::vector<std::vector<float>> ms(nv);
   std::vector<std::vector<uint8_t>> outs(nv, std::vector<uint8_t>((size_t)nb * 6));
   hipEvent_t e0, e1;
@@ -101,7 +112,7 @@ int main(int argc, char** argv) {
   for (int v = 0; v < nv; ++v) {
     if (!strstr(vs[v].name, filter)) continue;
     std::sort(ms[v].begin(), ms[v].end());
-    int ref = v < 6 ? 0 : 6;
+    int ref = strncmp(vs[v].name, "ref", 3) == 0 ? 0 : 6;
     bool same = outs[v] == outs[ref];
     double gbit = (double)nb * 40 / (ms[v][ms[v].size() / 2] * 1e-3) / 1e9;
     printf("%-18s median %.4f ms  min %.4f ms  %.1f Gbit/s  %s\n", vs[v].name, ms[v][ms[v].size() / 2],

@@ -46,7 +46,7 @@ def main():
     d_fetch, d_write = avg(fetch[dec_k[0]]), avg(write[dec_k[0]])
     traffic = d_fetch * read_scale + d_write * write_scale
     res = {
-        "workload_key": f"{opt.get('--code', 'k7')}:frames{opt.get('--frames', '16')}:{opt.get('--layout', 'block')}",
+        "workload_key": f"{opt.get('--code', 'k7')}:frames{opt.get('--frames', '64')}:{opt.get('--layout', 'block')}",
         "kernel": dec_k[0],
         "nblocks": nblocks,
         "raw_fetch_bytes_per_launch": d_fetch,
@@ -60,7 +60,7 @@ def main():
                 "FETCH_SIZE counts half of a wide streaming read on gfx950); Infinity-Cache hits are "
                 "counted by these L2-side counters",
     }
-    name = "pmc_traffic.json" if res["workload_key"] == "k7:frames16:block" else \
+    name = "pmc_traffic.json" if res["workload_key"] == "k7:frames64:block" else \
         f"pmc_traffic_{res['workload_key'].replace(':', '_')}.json"
     with open(os.path.join(root, name), "w") as f:
         json.dump(res, f, indent=1)

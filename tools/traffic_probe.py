@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(REPO, "convolutional-codes_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--code", default="k7")
-    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--layout", choices=("block", "step"), default="block")
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
