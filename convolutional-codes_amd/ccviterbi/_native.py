@@ -22,7 +22,7 @@ class CcvPlanDesc(ctypes.Structure):
     """ccv_plan_desc (include/ccv.h)."""
     _fields_ = [(name, ctypes.c_int) for name in (
         "channel", "n", "K", "blen", "gen_mode", "steps", "states", "info_bytes", "out_bytes",
-        "in_step_bytes", "kernel", "decision_word_bytes", "device")]
+        "in_step_bytes", "kernel", "decision_word_bytes", "device", "lanes")]
 
 
 _cache = {}

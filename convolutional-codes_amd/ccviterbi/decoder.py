@@ -15,7 +15,7 @@ import numpy as np
 from . import _native
 from .code import GEN_REF_X86, HARD, SOFT, Code
 
-KERNEL_REGISTER, KERNEL_GENERIC = 1, 2
+KERNEL_REGISTER, KERNEL_GENERIC, KERNEL_MULTILANE = 1, 2, 3
 FLAG_GENERIC = 1
 FLAG_STEP_MAJOR = 2
 
@@ -67,7 +67,8 @@ class Plan:
 
     @property
     def kernel(self):
-        return {KERNEL_REGISTER: "register", KERNEL_GENERIC: "generic"}[self.desc.kernel]
+        return {KERNEL_REGISTER: "register", KERNEL_GENERIC: "generic",
+                KERNEL_MULTILANE: "multilane"}[self.desc.kernel]
 
     def trellis(self) -> np.ndarray:
         out = np.zeros((self.desc.states, 2), np.uint8)

@@ -1,0 +1,301 @@
+// acs_multi.hpp -- register-trellis Viterbi for K = 8, 9 (128 / 256 states), specialised per code.
+//
+// L = 2^(K-7) lanes of one wave decode one block; every lane holds 64 path metrics in VGPRs, so the
+// register footprint and the ACS instruction stream match the K <= 7 kernel (acs_reg.hpp).
+//
+// Physical state numbering: phys = (q << 6) | r with q = lane within the block's lane group and
+// r = register. The ACS is done in place (the survivors of predecessors s, s|1 overwrite their
+// registers), so the logical meaning of the physical bits rotates by one position per step: at
+// phase p = t mod (K-1) the logical state held at phys is rotr_{K-1}(phys, p). The logical bit 0 --
+// the bit a butterfly pairs on -- is therefore a register bit for 6 of every K-1 steps (ordinary
+// in-lane butterflies) and a lane bit for the other K-7 steps. Those cross phases need no data
+// exchange: each lane reads its even and odd predecessor from the pair's two lanes with a quad_perm
+// DPP move and computes the one new state its position holds (input bit = its own lane bit).
+// Branch metrics depend on the lane bits, so each use takes BM[e(q)] where the expected symbol e(q)
+// per lane position is a compile-time tuple; the per-lane select is shared by common subexpressions.
+//
+// Exactness: the same adds, strict compare (sign of odd - even) and min as the reference
+// (AWGN-channel/viterbi-decoder.c:108-141); the lowest-index argmin and the traceback
+// (:71-90) work on logical state numbers.
+//
+// Decisions: each lane packs its 64 decision bits per step (bit r = register r), stored to
+// [T][P] 64-bit words, P = (nblocks * L) rounded up to 64, column = global lane index. The traceback
+// is run by all L lanes of a group in lockstep: each loads its own word (address independent of the
+// state) and fetches the word of lane q(state) with ds_bpermute.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "acs_reg.hpp"
+#include "trellis.hpp"
+
+namespace ccv {
+
+template <CodeSpec C>
+struct Multi {
+  static constexpr int n = C.K - 1;          // state bits
+  static constexpr int QB = C.K - 7;         // lane bits
+  static constexpr int L = 1 << QB;          // lanes per block
+  static constexpr int S = 1 << n;
+  static constexpr int NS = 1 << C.n;
+  static constexpr uint32_t rotr(uint32_t x, int p) {
+    p %= n;
+    return p == 0 ? x : (((x >> p) | (x << (n - p))) & (S - 1));
+  }
+  static constexpr uint32_t logical(int q, int r, int p) { return rotr(((uint32_t)q << 6) | (uint32_t)r, p); }
+};
+
+__device__ __forceinline__ uint32_t rotl_bits(uint32_t x, int k, int n) {
+  return k == 0 ? x : (((x << k) | (x >> (n - k))) & ((1u << n) - 1u));
+}
+__device__ __forceinline__ uint32_t rotr_bits(uint32_t x, int k, int n) {
+  return k == 0 ? x : (((x >> k) | (x << (n - k))) & ((1u << n) - 1u));
+}
+
+// Per-lane branch metric BM[e(q)] for a compile-time tuple e(0..L-1); qb0/qb1 = this lane's bits.
+template <int L, int E0, int E1, int E2, int E3, typename MT, int NS>
+__device__ __forceinline__ MT select_bm(const MT (&BM)[NS], bool qb0, bool qb1) {
+  if constexpr (L == 2) {
+    if constexpr (E0 == E1) return BM[E0];
+    else return qb0 ? BM[E1] : BM[E0];
+  } else {
+    if constexpr (E0 == E1 && E1 == E2 && E2 == E3) {
+      return BM[E0];
+    } else {
+      const MT lo = (E0 == E1) ? BM[E0] : (qb0 ? BM[E1] : BM[E0]);
+      const MT hi = (E2 == E3) ? BM[E2] : (qb0 ? BM[E3] : BM[E2]);
+      if constexpr (E0 == E2 && E1 == E3) return lo;
+      else return qb1 ? hi : lo;
+    }
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL, typename MT>
+__device__ __forceinline__ MT dpp(MT x) {
+  if constexpr (sizeof(MT) == 4 && std::is_same<MT, float>::value) return dpp_f32<CTRL>(x);
+  else return dpp_u32<CTRL>(x);
+}
+
+// One new-state computation (cross phase) or one butterfly (in-lane phase) for register R, in place.
+// In-lane phase P: butterfly (R, R | 1 << P); the i = 0 survivor's decision is shifted into `lo`,
+// the i = 1 survivor's into `hi`, so bit compress_P(R) of lo / hi belongs to register R / R | 1 << P.
+// Cross phase: the decision of register R goes to bit R of (hi:lo).
+template <CodeSpec C, int P, int R, bool SAT, typename MT>
+__device__ __forceinline__ void multi_acs(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0, bool qb1,
+                                          uint32_t& lo, uint32_t& hi) {
+  using X = Multi<C>;
+  constexpr int L = X::L;
+  auto sat = [](MT v) {
+    if constexpr (SAT) return vmin(v, (MT)0xFF00);   // binary-symmetric-channel/viterbi-decoder.c:127-130
+    else return v;
+  };
+  if constexpr (P < 6) {
+    if constexpr ((R & (1 << P)) == 0) {
+      constexpr int R1 = R | (1 << P);
+      constexpr auto e = [](int q, int odd, int in) {
+        return expected_symbol(C, X::logical(q, R, P) | (uint32_t)odd, in);
+      };
+      const MT a0 = sat(M[R] + select_bm<L, e(0, 0, 0), e(1 % L, 0, 0), e(2 % L, 0, 0), e(3 % L, 0, 0)>(BM, qb0, qb1));
+      const MT a1 = sat(M[R1] + select_bm<L, e(0, 1, 0), e(1 % L, 1, 0), e(2 % L, 1, 0), e(3 % L, 1, 0)>(BM, qb0, qb1));
+      const MT b0 = sat(M[R] + select_bm<L, e(0, 0, 1), e(1 % L, 0, 1), e(2 % L, 0, 1), e(3 % L, 0, 1)>(BM, qb0, qb1));
+      const MT b1 = sat(M[R1] + select_bm<L, e(0, 1, 1), e(1 % L, 1, 1), e(2 % L, 1, 1), e(3 % L, 1, 1)>(BM, qb0, qb1));
+      M[R] = vmin(a0, a1);
+      lo = shift_in(lo, a0, a1);
+      M[R1] = vmin(b0, b1);
+      hi = shift_in(hi, b0, b1);
+    }
+  } else {
+    // cross-lane butterfly on lane bit B: even predecessor in the lane with bit B clear, odd in the
+    // lane with it set, same register; this lane's new state has input bit = its own bit B
+    constexpr int B = P - 6;
+    constexpr int CE = B == 0 ? 0xA0 : 0x44;   // quad_perm [0,0,2,2] / [0,1,0,1]
+    constexpr int CO = B == 0 ? 0xF5 : 0xEE;   // quad_perm [1,1,3,3] / [2,3,2,3]
+    constexpr auto e = [](int q, int odd) {
+      const int qe = q & ~(1 << B);
+      return expected_symbol(C, X::logical(qe, R, P) | (uint32_t)odd, (q >> B) & 1);
+    };
+    const MT E = dpp<CE, MT>(M[R]);
+    const MT O = dpp<CO, MT>(M[R]);
+    const MT a0 = sat(E + select_bm<L, e(0, 0), e(1 % L, 0), e(2 % L, 0), e(3 % L, 0)>(BM, qb0, qb1));
+    const MT a1 = sat(O + select_bm<L, e(0, 1), e(1 % L, 1), e(2 % L, 1), e(3 % L, 1)>(BM, qb0, qb1));
+    M[R] = vmin(a0, a1);
+    if constexpr (R >= 32) hi = shift_in(hi, a0, a1);
+    else lo = shift_in(lo, a0, a1);
+  }
+}
+
+template <CodeSpec C, int P, bool SAT, typename MT, size_t... I>
+__device__ __forceinline__ uint64_t multi_step_impl(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0,
+                                                    bool qb1, std::index_sequence<I...>) {
+  uint32_t lo = 0, hi = 0;
+  (multi_acs<C, P, 63 - (int)I, SAT, MT>(M, BM, qb0, qb1, lo, hi), ...);   // descending registers
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <CodeSpec C, int P, bool SAT, typename MT>
+__device__ __forceinline__ uint64_t multi_step(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0, bool qb1) {
+  return multi_step_impl<C, P, SAT, MT>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
+}
+
+// Bit of register r's decision in the word stored at phase p (see multi_acs).
+__device__ __forceinline__ uint32_t multi_dec_pos(uint32_t r, int p) {
+  if (p >= 6) return r;
+  const uint32_t low = r & ((1u << p) - 1u);
+  return (((r >> p) & 1u) << 5) | ((r >> (p + 1)) << p) | low;
+}
+
+// One period (phases 0..n-1) of steps t .. t+n-1, each guarded by t + P < T; slot P of the input
+// ring is consumed by phase P and refilled with step t + P + n.
+template <CodeSpec C, bool SAT, typename MT, int P, class In, class Load, class Metrics>
+__device__ __forceinline__ void multi_period(int t, int T, MT (&M)[64], In (&ring)[Multi<C>::n],
+                                             Load& load, Metrics& metrics, uint64_t* dec,
+                                             size_t dstride, bool qb0, bool qb1) {
+  if constexpr (P < Multi<C>::n) {
+    constexpr int n = Multi<C>::n;
+    if (t + P < T) {
+      MT BM[1 << C.n];
+      metrics(ring[P], BM);
+      dec[(size_t)(t + P) * dstride] = multi_step<C, P, SAT, MT>(M, BM, qb0, qb1);
+    }
+    const int tn = t + P + n;
+    ring[P] = load(tn < T ? tn : T - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    multi_period<C, SAT, MT, P + 1>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+  }
+}
+
+// Lowest logical index among the group's minima (reference traceback :72-79).
+template <CodeSpec C, typename MT>
+__device__ __forceinline__ uint32_t multi_argmin(const MT (&M)[64], int phase, int q, MT sentinel,
+                                                 MT& best) {
+  using X = Multi<C>;
+  best = sentinel;
+  uint32_t idx = 0xFFFFFFFFu;
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    const uint32_t li = rotr_bits(((uint32_t)q << 6) | (uint32_t)r, phase, X::n);
+    const bool better = M[r] < best || (M[r] == best && idx != 0xFFFFFFFFu && li < idx);
+    best = better ? M[r] : best;
+    idx = better ? li : idx;
+  }
+#pragma unroll
+  for (int off = 1; off < X::L; off <<= 1) {
+    const MT ob = __shfl_xor(best, off, 64);
+    const uint32_t oi = (uint32_t)__shfl_xor((int)idx, off, 64);
+    const bool better = ob < best || (ob == best && oi < idx);
+    best = better ? ob : best;
+    idx = better ? oi : idx;
+  }
+  return idx == 0xFFFFFFFFu ? 0u : idx;   // nothing below the sentinel: state 0 as the reference
+}
+
+template <CodeSpec C>
+__device__ __forceinline__ uint32_t multi_traceback(const RegArgs& a, int blk, uint32_t st, bool writer) {
+  using X = Multi<C>;
+  const int T = a.T, OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+  const int lane = threadIdx.x & 63;
+  const int gbase = lane & ~(X::L - 1);
+  const uint64_t* dec = reinterpret_cast<const uint64_t*>(a.dec) + (size_t)blockIdx.x * kRegThreads + lane;
+  const size_t stride = (size_t)a.dec_stride;
+  uint32_t errors = 0;
+  for (int lo = (T - 1) & ~7; lo >= 0; lo -= 8) {
+    uint64_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = dec[(size_t)(lo + k < T ? lo + k : T - 1) * stride];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+      const int t = lo + k;
+      if (t < T) {
+        const int ph = t % X::n;   // survivors of step t sit at the phase-(t+1) positions
+        const uint32_t phys = rotl_bits(st, ph + 1 == X::n ? 0 : ph + 1, X::n);
+        const int src = (gbase + (int)(phys >> 6)) << 2;
+        const uint32_t pos = multi_dec_pos(phys & 63u, ph);
+        const uint32_t wl = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)w[k]);
+        const uint32_t wh = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(w[k] >> 32));
+        const uint32_t bit = ((pos < 32 ? wl : wh) >> (pos & 31)) & 1u;
+        acc |= (st >> (C.K - 2)) << (7 - k);
+        st = ((st << 1) & (X::S - 1)) | bit;
+      }
+    }
+    if (writer) {
+      a.out[(size_t)blk * OB + (lo >> 3)] = (uint8_t)acc;
+      if (a.info != nullptr && (lo >> 3) < IB) {
+        int valid = a.blen - lo;
+        valid = valid > 8 ? 8 : valid;
+        const uint32_t mask = (0xFFu << (8 - valid)) & 0xFFu;
+        errors += __builtin_popcount((acc ^ a.info[(size_t)blk * IB + (lo >> 3)]) & mask);
+      }
+    }
+  }
+  return errors;
+}
+
+// HARD = false: soft input float [nb][T][2^n]; HARD = true: symbols uint8 [nb][T].
+template <CodeSpec C, bool HARD>
+__global__ __launch_bounds__(kRegThreads) void viterbi_multi(RegArgs a) {
+  using X = Multi<C>;
+  using MT = typename std::conditional<HARD, uint32_t, float>::type;
+  constexpr int NS = X::NS;
+  const int lane = threadIdx.x;
+  const int q = lane & (X::L - 1);
+  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  const int blk = (blockIdx.x * kRegThreads + lane) / X::L;
+  const int T = a.T, nb = a.nblocks;
+  const int bc = blk < nb ? blk : nb - 1;
+  uint64_t* dec = reinterpret_cast<uint64_t*>(a.dec) + (size_t)blockIdx.x * kRegThreads + lane;
+  const size_t dstride = (size_t)a.dec_stride;
+  MT M[64];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    if constexpr (HARD) M[r] = (q == 0 && r == 0) ? 0u : 0xFF00u;
+    else M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
+  }
+  constexpr int n = X::n;
+  if constexpr (HARD) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(a.in) + (size_t)bc * T;
+    auto load = [&](int t) { return (uint32_t)p[t]; };
+    auto metrics = [](uint32_t sym, MT (&BM)[NS]) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) BM[k] = __builtin_popcount((uint32_t)k ^ (sym & (uint32_t)(NS - 1)));
+    };
+    uint32_t ring[n];
+#pragma unroll
+    for (int k = 0; k < n; ++k) ring[k] = load(k < T ? k : T - 1);
+    // saturation (reference :127-130) only matters while some states are unreachable: period 0
+    multi_period<C, true, MT, 0>(0, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+    for (int t = n; t < T; t += n)
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+  } else {
+    const float* p = reinterpret_cast<const float*>(a.in) + (size_t)bc * T * NS;
+    auto load = [&](int t) { return load_soft_step<NS>(p + (size_t)t * NS); };
+    auto metrics = [](const SoftStep<NS>& in, MT (&BM)[NS]) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) BM[k] = in.v[k];
+    };
+    SoftStep<NS> ring[n];
+#pragma unroll
+    for (int k = 0; k < n; ++k) ring[k] = load(k < T ? k : T - 1);
+    for (int t = 0; t < T; t += n)
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+  }
+  MT best;
+  const MT sentinel = HARD ? (MT)0xFF00u : (MT)__builtin_inff();
+  const uint32_t st = multi_argmin<C, MT>(M, T % X::n, q, sentinel, best);
+  const bool writer = q == 0 && blk < nb;
+  if constexpr (HARD) {
+    if (writer && a.path_metric) a.path_metric[blk] = (int32_t)best;
+  }
+  const uint32_t errors = multi_traceback<C>(a, blk, st, writer);
+  accumulate_errors(a, errors);
+}
+
+}  // namespace ccv

@@ -61,7 +61,8 @@ struct ccv_plan {
   ccv_plan_desc d{};
   uint64_t polys[ccv::kMaxN] = {};
   std::vector<uint8_t> exp;          // [S][2]
-  int reg_index = -1;                // kRegCodes index, or -1 for the generic kernel
+  int reg_index = -1;                // kRegCodes index, or -1
+  int multi_index = -1;              // kMultiCodes index (K = 8, 9), or -1
   bool step_major = false;           // soft input layout [T][nblocks][2^n] (CCV_FLAG_STEP_MAJOR)
   int generic_spt = 1, generic_threads = 64, generic_chunk = 1;
   size_t generic_lds = 0;
@@ -73,13 +74,17 @@ struct ccv_plan {
 
 namespace {
 
-size_t padded_blocks(size_t nblocks) {
-  return (nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads * ccv::kRegThreads;
+// Decision columns: one per wave lane (nblocks * lanes), rounded up to whole waves.
+size_t padded_columns(const ccv_plan& p, size_t nblocks) {
+  const size_t cols = nblocks * (size_t)p.d.lanes;
+  return (cols + ccv::kRegThreads - 1) / ccv::kRegThreads * ccv::kRegThreads;
 }
 
 size_t decision_bytes(const ccv_plan& p, size_t nblocks) {
-  return padded_blocks(nblocks) * (size_t)p.d.steps * (size_t)p.d.decision_word_bytes;
+  return padded_columns(p, nblocks) * (size_t)p.d.steps * (size_t)p.d.decision_word_bytes;
 }
+
+bool register_path(const ccv_plan& p) { return p.reg_index >= 0 || p.multi_index >= 0; }
 
 int find_reg_kernel(const ccv_plan& p) {
   using namespace ccv;
@@ -87,6 +92,19 @@ int find_reg_kernel(const ccv_plan& p) {
   std::vector<uint8_t> tab(2 * (size_t)S);
   for (size_t i = 0; i < kNumRegCodes; ++i) {
     const CodeSpec& c = kRegCodes[i];
+    if (c.n != p.d.n || c.K != p.d.K) continue;
+    build_trellis(c.n, c.K, c.poly, c.gen, tab.data());
+    if (tab == p.exp) return (int)i;
+  }
+  return -1;
+}
+
+int find_multi_kernel(const ccv_plan& p) {
+  using namespace ccv;
+  const int S = 1 << (p.d.K - 1);
+  std::vector<uint8_t> tab(2 * (size_t)S);
+  for (size_t i = 0; i < kNumMultiCodes; ++i) {
+    const CodeSpec& c = kMultiCodes[i];
     if (c.n != p.d.n || c.K != p.d.K) continue;
     build_trellis(c.n, c.K, c.poly, c.gen, tab.data());
     if (tab == p.exp) return (int)i;
@@ -173,13 +191,19 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
     return fail("step-major input is a soft-decision layout");
   }
   p->reg_index = (flags & CCV_FLAG_GENERIC) ? -1 : find_reg_kernel(*p);
+  p->multi_index = (flags & CCV_FLAG_GENERIC) || p->reg_index >= 0 ? -1 : find_multi_kernel(*p);
   if (p->step_major && p->reg_index < 0) {
     delete p;
-    return fail("step-major input needs a register-trellis code");
+    return fail("step-major input needs a register-trellis code with K <= 7");
   }
+  p->d.lanes = 1;
   if (p->reg_index >= 0) {
     p->d.kernel = CCV_KERNEL_REGISTER;
     p->d.decision_word_bytes = p->d.states > 32 ? 8 : 4;
+  } else if (p->multi_index >= 0) {
+    p->d.kernel = CCV_KERNEL_MULTILANE;
+    p->d.decision_word_bytes = 8;
+    p->d.lanes = 1 << (K - 7);
   } else {
     const int S = p->d.states;
     p->d.kernel = CCV_KERNEL_GENERIC;
@@ -237,7 +261,7 @@ int ccv_plan_trellis(const ccv_plan* p, uint8_t* exp) {
 
 int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {
   if (!p) return fail("null plan");
-  if (p->reg_index < 0) return 0;
+  if (!register_path(*p)) return 0;
   return p->dec.grow(decision_bytes(*p, max_blocks), p->stream);
 }
 
@@ -250,13 +274,15 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
   if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
   hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
   const bool hard = p->d.channel == CCV_HARD;
-  if (p->reg_index >= 0) {
+  if (register_path(*p)) {
+    if (d_decisions && p->reg_index < 0)
+      return fail("decision export needs the single-lane register kernel (K <= 7)");
     ccv::RegArgs a{};
     a.in = d_in;
     a.T = p->d.steps;
     a.nblocks = (int)nblocks;
     a.blen = p->d.blen;
-    a.dec_stride = (int)padded_blocks(nblocks);
+    a.dec_stride = (int)padded_columns(*p, nblocks);
     a.out = d_out;
     a.path_metric = hard ? d_path_metric : nullptr;
     a.info = d_info;
@@ -267,10 +293,14 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
       if (p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
       a.dec = p->dec.ptr;
     }
-    const int grid = (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads);
-    const ccv::RegLaunchFn* fns =
-        hard ? ccv::hard_reg_launchers() : ccv::soft_reg_launchers(p->step_major);
-    HIP_TRY(fns[p->reg_index](a, grid, stream));
+    const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
+    if (p->reg_index >= 0) {
+      const ccv::RegLaunchFn* fns =
+          hard ? ccv::hard_reg_launchers() : ccv::soft_reg_launchers(p->step_major);
+      HIP_TRY(fns[p->reg_index](a, grid, stream));
+    } else {
+      HIP_TRY(ccv::multi_launchers(hard)[p->multi_index](a, grid, stream));
+    }
   } else {
     if (d_decisions) return fail("decision export needs the register kernel");
     ccv::GenericArgs a{};

@@ -34,8 +34,19 @@ inline constexpr CodeSpec kRegCodes[] = {
 };
 inline constexpr size_t kNumRegCodes = sizeof(kRegCodes) / sizeof(kRegCodes[0]);
 
+// Codes with 128 / 256 states: multi-lane register kernel (acs_multi.hpp), 2 / 4 lanes per block.
+inline constexpr CodeSpec kMultiCodes[] = {
+    // K=8 (371,247)_8 and K=9 (561,753)_8 (BASELINE.json config 3)
+    CCV_CODE2(8, 0xF900000000000000, 0xA700000000000000, GEN_REF_X86),
+    CCV_CODE2(8, 0xF900000000000000, 0xA700000000000000, GEN_TRUE_PARITY),
+    CCV_CODE2(9, 0xB880000000000000, 0xF580000000000000, GEN_REF_X86),
+    CCV_CODE2(9, 0xB880000000000000, 0xF580000000000000, GEN_TRUE_PARITY),
+};
+inline constexpr size_t kNumMultiCodes = sizeof(kMultiCodes) / sizeof(kMultiCodes[0]);
+
 using RegLaunchFn = hipError_t (*)(const RegArgs&, int grid, hipStream_t stream);
 const RegLaunchFn* soft_reg_launchers(bool step_major);   // [kNumRegCodes], reg_soft.hip
 const RegLaunchFn* hard_reg_launchers();   // [kNumRegCodes], reg_hard.hip
+const RegLaunchFn* multi_launchers(bool hard);   // [kNumMultiCodes], reg_multi.hip
 
 }  // namespace ccv

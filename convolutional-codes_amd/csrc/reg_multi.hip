@@ -1,0 +1,30 @@
+// reg_multi.hip -- ahead-of-time instantiation of the multi-lane register-trellis kernel
+// (acs_multi.hpp) for the K = 8 and K = 9 codes, soft and hard decision.
+#include <array>
+#include <utility>
+
+#include "acs_multi.hpp"
+#include "reg_codes.hpp"
+
+namespace ccv {
+namespace {
+
+template <size_t I, bool HARD>
+hipError_t launch(const RegArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL((viterbi_multi<kMultiCodes[I], HARD>), dim3(grid), dim3(kRegThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <bool HARD, size_t... I>
+constexpr std::array<RegLaunchFn, sizeof...(I)> make(std::index_sequence<I...>) {
+  return {&launch<I, HARD>...};
+}
+
+constexpr auto kSoft = make<false>(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kHard = make<true>(std::make_index_sequence<kNumMultiCodes>{});
+
+}  // namespace
+
+const RegLaunchFn* multi_launchers(bool hard) { return hard ? kHard.data() : kSoft.data(); }
+
+}  // namespace ccv

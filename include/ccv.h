@@ -41,6 +41,7 @@ extern "C" {
 
 #define CCV_KERNEL_REGISTER 1 /* code-specialised register-trellis kernel                       */
 #define CCV_KERNEL_GENERIC 2  /* table-driven LDS kernel                                        */
+#define CCV_KERNEL_MULTILANE 3 /* K = 8, 9: register-trellis kernel, 2^(K-7) lanes per block      */
 
 typedef struct ccv_plan ccv_plan;
 
@@ -52,8 +53,9 @@ typedef struct {
     int out_bytes;       /* OB */
     int in_step_bytes;   /* 4 * 2^n (soft) or 1 (hard) */
     int kernel;          /* CCV_KERNEL_* */
-    int decision_word_bytes; /* register kernel: bytes of one step's decisions per block */
+    int decision_word_bytes; /* register kernels: bytes of one decision word */
     int device;
+    int lanes;           /* wave lanes (decision words per step) per block: 1, or 2^(K-7) multilane */
 } ccv_plan_desc;
 
 /* A plan binds a code to the device that is current on the calling thread.
@@ -73,8 +75,8 @@ int ccv_plan_reserve(ccv_plan* plan, size_t max_blocks);
  * legacy default stream).  d_path_metric (hard only), d_info + d_errors (error counting: adds the
  * batch's bit errors over the first blen bits to *d_errors) and d_decisions (register kernel only:
  * [T][P] words of ccv_plan_desc.decision_word_bytes, P = nblocks rounded up to a multiple of 64,
- * block b in column b; bit s set = the survivor into state s came from the odd predecessor) may be
- * NULL. */
+ * block b in column b; bit s set = the survivor into state s came from the odd predecessor; not
+ * available for the multilane kernel, whose words are in its physical state order) may be NULL. */
 int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t* d_out,
                       int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
                       void* d_decisions, void* stream);

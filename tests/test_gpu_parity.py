@@ -65,7 +65,14 @@ def test_register_kernel_selected_for_benchmark_codes():
     for c in (K7, K7.with_(gen_mode=GEN_TRUE_PARITY), CODEBOOK[0], CODEBOOK[3], CODEBOOK[5]):
         assert Plan(c, SOFT).kernel == "register"
         assert Plan(c, HARD).kernel == "register"
-    assert Plan(K9, SOFT).kernel == "generic"
+    for c in (K8, K9):
+        for gen in (GEN_REF_X86, GEN_TRUE_PARITY):
+            for channel in (SOFT, HARD):
+                plan = Plan(c.with_(gen_mode=gen), channel)
+                assert plan.kernel == "multilane" and plan.desc.lanes == 1 << (c.K - 7)
+        assert Plan(c, SOFT, FLAG_GENERIC).kernel == "generic"
+    # a K=9 code without an ahead-of-time kernel falls back to the table-driven kernel
+    assert Plan(Code(2, 9, 40, (0xF080000000000000, 0xA980000000000000)), SOFT).kernel == "generic"
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if c["name"] in (
@@ -126,9 +133,10 @@ def test_reference_api_generator_mode_true_parity():
 SEEDED = [
     ("k7_ref_soft", K7, SOFT), ("k7_true_soft", K7.with_(gen_mode=GEN_TRUE_PARITY), SOFT),
     ("k7_ref_hard", K7, HARD), ("k7_true_hard", K7.with_(gen_mode=GEN_TRUE_PARITY), HARD),
-    ("k8_soft", K8, SOFT), ("k8_true_hard", K8.with_(gen_mode=GEN_TRUE_PARITY), HARD),
+    ("k8_soft", K8, SOFT), ("k8_true_soft", K8.with_(gen_mode=GEN_TRUE_PARITY), SOFT),
+    ("k8_hard", K8, HARD), ("k8_true_hard", K8.with_(gen_mode=GEN_TRUE_PARITY), HARD),
     ("k9_soft", K9, SOFT), ("k9_true_soft", K9.with_(gen_mode=GEN_TRUE_PARITY), SOFT),
-    ("k9_hard", K9, HARD),
+    ("k9_hard", K9, HARD), ("k9_true_hard", K9.with_(gen_mode=GEN_TRUE_PARITY), HARD),
     ("code1_true_soft", CODEBOOK[1].with_(gen_mode=GEN_TRUE_PARITY), SOFT),
     ("code2_true_hard", CODEBOOK[2].with_(gen_mode=GEN_TRUE_PARITY), HARD),
     ("code3_true_soft", CODEBOOK[3].with_(gen_mode=GEN_TRUE_PARITY), SOFT),
@@ -163,6 +171,43 @@ def test_ragged_batches(nb):
     assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
 
 
+MULTI_SHAPES = [(1, 40), (3, 1), (15, 7), (16, 8), (17, 9), (33, 249), (100, 255), (257, 23)]
+
+
+@pytest.mark.parametrize("K", [8, 9])
+@pytest.mark.parametrize("nb,blen", MULTI_SHAPES, ids=[f"nb{a}_blen{b}" for a, b in MULTI_SHAPES])
+def test_multilane_shapes(K, nb, blen):
+    """Multilane kernel: ragged batches (lane groups straddling waves) and every T mod (K-1) phase
+    the final argmin and the traceback start from (T = blen + K - 1)."""
+    c = (K8 if K == 8 else K9).with_(blen=blen)
+    info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), nb * 7 + blen)
+    plan = Plan(c, SOFT)
+    assert plan.kernel == "multilane"
+    assert np.array_equal(plan.decode_host(rx), O.viterbi_soft(_ocode(c), rx))
+    info, syms = ch.bsc_blocks(c, nb, 90000, nb * 5 + blen)
+    out, pm = Plan(c, HARD).decode_host(syms)
+    ref, ref_pm = O.viterbi_hard(_ocode(c), syms)
+    assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+
+
+def test_multilane_error_count_and_no_decision_export(torch_cuda):
+    torch = torch_cuda
+    c = K9.with_(gen_mode=GEN_TRUE_PARITY)
+    nb = 2000
+    info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 99)
+    plan = Plan(c, SOFT)
+    d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    plan.decode_device(_device(torch, rx), nb, d_out, d_info=_device(torch, info), d_errors=d_err)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
+    assert int(d_err.item()) == ch.count_bit_errors(c, info, out)
+    d_dec = torch.empty((c.steps, 4 * nb + 64), dtype=torch.int64, device="cuda")
+    with pytest.raises(Exception, match="single-lane"):
+        plan.decode_device(_device(torch, rx), nb, d_out, d_decisions=d_dec)
+
+
 def test_empty_batch_is_noop(torch_cuda):
     torch = torch_cuda
     plan = Plan(K7, SOFT)
@@ -175,6 +220,8 @@ EDGE = [
     ("k7_blen255", K7.with_(blen=255), SOFT),            # T = 261 > the reference encoder's 255
     ("k7_blen1", K7.with_(blen=1), SOFT),
     ("k2", Code(2, 2, 40, (0xC000000000000000, 0x8000000000000000)), SOFT),
+    ("k9_blen255", K9.with_(blen=255), SOFT),
+    ("k8_blen255_hard", K8.with_(blen=255), HARD),
     ("k12", Code(2, 12, 60, (0xFFD0000000000000, 0xB970000000000000)), SOFT),
     ("k12_hard", Code(2, 12, 60, (0xFFD0000000000000, 0xB970000000000000)), HARD),
     ("n1_k5", Code(1, 5, 40, (0xF800000000000000,)), SOFT),
@@ -208,7 +255,7 @@ def test_edge_codes(name, c, channel):
 def test_negative_and_tied_soft_metrics():
     """General float inputs: negative metrics and exact ties follow the reference's strict '<'."""
     rng = np.random.default_rng(3)
-    for c in (K7, CODEBOOK[0], K9):
+    for c in (K7, CODEBOOK[0], K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
         data = rng.integers(-3, 4, size=(300, c.steps, 4)).astype(np.float32)  # many exact ties
         for flags in (0, FLAG_GENERIC):
             assert np.array_equal(Plan(c, SOFT, flags).decode_host(data), O.viterbi_soft(_ocode(c), data))
@@ -223,13 +270,14 @@ def _device(torch, arr):
     return torch.from_numpy(np.ascontiguousarray(arr)).to("cuda")
 
 
+@pytest.mark.parametrize("base", [K7, K9], ids=["k7", "k9"])
 @pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY])
-def test_full_frame_noiseless(torch_cuda, gen):
+def test_full_frame_noiseless(torch_cuda, gen, base):
     """True parity: (171,133) is a proper non-catastrophic code, so a noiseless frame decodes with
     zero errors. The x86-idiom variant is not injective (some butterflies emit the same symbol for
     both inputs), so even noiseless frames keep errors -- there the check is equality with the oracle."""
     torch = torch_cuda
-    c = K7.with_(gen_mode=gen)
+    c = base.with_(gen_mode=gen)
     info, rx = ch.awgn_blocks(c, FRAME, 0.0, 2024)
     plan = Plan(c, SOFT)
     d_out = torch.empty((FRAME, c.out_bytes), dtype=torch.uint8, device="cuda")
