@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0xC0DE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline work budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fused-channel", action="store_true",
+                    help="skip the informational on-device channel + decode measurement")
     args = ap.parse_args()
 
     import torch
@@ -171,6 +173,8 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
 
+    errs = d_err.clone()   # the timed steps' error count (the informational runs below add more)
+
     # informational, outside the timed region: the same batch staged from pinned host memory
     # (H2D + decode + D2H of the decoded bits), i.e. the PCIe-inclusive rate
     pcie_s = None
@@ -187,8 +191,29 @@ def main():
         torch.cuda.synchronize()
         pcie_s = (time.perf_counter() - t1) / reps
 
+    # informational: the same frames generated AND decoded on the GPU (ccv_simulate_device, the
+    # on-device channel of SURVEY.md 8(f) #1) -- no host producer, no input in HBM
+    fused = None
+    if rank == 0 and not args.no_fused_channel:
+        d_ferr = torch.zeros(1, dtype=torch.int64, device="cuda")
+        scaling = ch.noise_scaling(args.ebn0)
+        plan.simulate_device(args.seed, 0, nb, scaling, d_errors=d_ferr, stream=stream)   # warm-up
+        d_ferr.zero_()
+        reps = 5
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        for _ in range(reps):
+            plan.simulate_device(args.seed, 0, nb, scaling, d_errors=d_ferr, stream=stream)
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        f_ms = ev[0].elapsed_time(ev[1]) / reps
+        f_err = int(d_ferr.item()) // reps
+        fused = {"mbit_s": round(nb * code.blen / (f_ms * 1e-3) / 1e6, 1), "kernel_ms": round(f_ms, 4),
+                 "ber": f_err / (nb * code.blen),
+                 "note": "same Philox frames generated on the GPU (encoder, mapper, Box-Muller AWGN, "
+                         "demapper fused ahead of the ACS)"}
+
     counters = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
-    errs = d_err.clone()
     if world > 1:
         dist.all_reduce(counters, op=dist.ReduceOp.MAX)
         dist.all_reduce(errs, op=dist.ReduceOp.SUM)   # the BER counter reduction (RCCL over xGMI)
@@ -247,6 +272,7 @@ def main():
                 "bytes_per_launch": int(bytes_per_launch),
             },
             "cpu_baseline": cpu,
+            "fused_channel": fused,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -60,6 +60,8 @@ def core():
     L.ccv_plan_reserve.restype = _i
     L.ccv_decode_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
     L.ccv_decode_device.restype = _i
+    L.ccv_simulate_device.argtypes = [_vp, _u64, _u64, _sz, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.ccv_simulate_device.restype = _i
     L.ccv_decode_host.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.ccv_decode_host.restype = _i
     L.ccv_device_count.argtypes = []

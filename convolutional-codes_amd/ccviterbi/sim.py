@@ -88,22 +88,56 @@ class GpuFrameDecoder:
         return int(self.d_err.item())
 
 
+class DeviceChannelDecoder:
+    """Frames generated AND decoded on the current GPU (ccv_simulate_device): the same Philox frames
+    as the host producers, no host generation and no input traffic."""
+
+    def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None):
+        import torch
+
+        from .decoder import Plan
+        self.torch = torch
+        self.device = torch.device(device if device is not None else "cuda")
+        self.plan = Plan(code, channel)
+        self.plan.reserve(frame_blocks)
+        self.channel, self.frame_blocks, self.seed = channel, frame_blocks, seed
+        self.d_err = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+    def __call__(self, point: float, first_blocks: Sequence[int]) -> int:
+        """Bit errors of the frames starting at `first_blocks` at Eb/N0 (dB) or p_ppm `point`."""
+        param = ch.noise_scaling(point) if self.channel == SOFT else int(point)
+        self.d_err.zero_()
+        stream = self.torch.cuda.current_stream(self.device)
+        for first in first_blocks:
+            self.plan.simulate_device(self.seed, first, self.frame_blocks, param, d_errors=self.d_err,
+                                      stream=stream)
+        return int(self.d_err.item())
+
+
 def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
               bits_per_point: Optional[Callable[[float], int]] = None, frame_blocks: int = 25000,
               seed: int = 0xC0DE, rank: int = 0, world: int = 1,
               decode: Optional[Callable[[np.ndarray, np.ndarray], int]] = None,
-              threads: Optional[int] = None, reduce: bool = True) -> List[BerPoint]:
-    """BER at each point; `decode(info, data) -> errors` defaults to the GPU decoder."""
+              threads: Optional[int] = None, reduce: bool = True,
+              device_channel: bool = False) -> List[BerPoint]:
+    """BER at each point; `decode(info, data) -> errors` defaults to the GPU decoder. With
+    device_channel the frames are generated on the GPU as well (DeviceChannelDecoder)."""
     if bits_per_point is None:
         if channel == SOFT:
             bits_per_point = lambda p: reference_awgn_bits(p, code.blen)   # noqa: E731
         else:
             bits_per_point = lambda p: reference_bsc_bits(int(p), code.blen)  # noqa: E731
-    if decode is None:
+    dev = DeviceChannelDecoder(code, channel, frame_blocks, seed) if device_channel else None
+    if decode is None and dev is None:
         decode = GpuFrameDecoder(code, channel, frame_blocks)
     counters = np.zeros((len(points), 2), np.int64)
     for pi, p in enumerate(points):
         nframes = max(1, math.ceil(bits_per_point(p) / (frame_blocks * code.blen)))
+        if dev is not None:
+            mine = range(rank, nframes, world)
+            counters[pi, 0] += dev(p, [(pi << 40) + f * frame_blocks for f in mine])
+            counters[pi, 1] += len(mine) * frame_blocks * code.blen
+            continue
         for f in range(rank, nframes, world):
             first = (pi << 40) + f * frame_blocks
             if channel == SOFT:

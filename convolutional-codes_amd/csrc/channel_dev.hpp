@@ -1,0 +1,322 @@
+// channel_dev.hpp -- on-device channel producers fused ahead of the register-trellis ACS
+// (SURVEY.md section 8(f) #1): info bytes, encoder, mapper, AWGN (Box-Muller on Philox4x32-10) and
+// demapper -- or the BSC bit flips -- generated per lane, step by step, in the order the decoder
+// consumes them, so no channel data touches HBM. The draw sequence is the product's host Philox
+// producer's (csrc/sim.cpp PhiloxSource / Gauss / awgn_block / bsc_block), which follows the
+// reference drivers' rand() call order:
+//   AWGN-channel/main.c:217-223 (info bytes, rand() % 256), :93-106 (per symbol: map, add
+//   scaling * gengauss() per I/Q in double, demap); common/gaussian.c:18-38 (Box-Muller, cosine
+//   half first, u1 == 0 redrawn); common/demapper.c:61-70 (squared distance / ndist in fp32);
+//   binary-symmetric-channel/main.c:57-72 (per bit: rand() % 1000000 < p_ppm flips it).
+// Info bits, symbols and BSC flips are bit-identical to the host producer. The AWGN samples use the
+// device libm (ocml) log/sin/cos instead of glibc's, so a sample may differ in the last place where
+// the two libraries round differently (tests/test_gpu_parity.py measures how often).
+// Compiled with -ffp-contract=off: x + scaling * g and dx*dx + dy*dy must not fuse.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "acs_multi.hpp"
+#include "acs_reg.hpp"
+#include "trellis.hpp"
+
+namespace ccv {
+
+struct ChanArgs {
+  RegArgs r;                 // r.in unused; r.info = info_out (read back by the traceback)
+  uint64_t seed;
+  uint64_t first_block;      // block b of the batch is stream block first_block + b
+  float scaling;             // AWGN: noise scaling (AWGN-channel/main.c:157-161)
+  int32_t p_ppm;             // BSC: flip probability in ppm
+  uint8_t* info_out;         // [nb][IB] transmitted info bytes (required)
+  void* ch_out;              // optional export: soft float [nb][T][2^n] / hard uint8 [nb][T]
+};
+
+// Philox4x32-10 with one counter stream per block (key = seed, counter = (block, draw, 0, tag)).
+struct Philox {
+  uint32_t k0, k1, c0, c1, c2;
+  uint32_t b0, b1, b2, b3;
+  int used;
+  __device__ __forceinline__ void init(uint64_t seed, uint64_t block) {
+    k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32);
+    c0 = (uint32_t)block; c1 = (uint32_t)(block >> 32); c2 = 0;
+    used = 4;
+  }
+  __device__ __forceinline__ void refill() {
+    uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = 0x43435631u, y0 = k0, y1 = k1;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const uint32_t h0 = __umulhi(0xD2511F53u, x0), l0 = 0xD2511F53u * x0;
+      const uint32_t h1 = __umulhi(0xCD9E8D57u, x2), l1 = 0xCD9E8D57u * x2;
+      x0 = h1 ^ x1 ^ y0; x1 = l1;
+      x2 = h0 ^ x3 ^ y1; x3 = l0;
+      y0 += 0x9E3779B9u; y1 += 0xBB67AE85u;
+    }
+    b0 = x0; b1 = x1; b2 = x2; b3 = x3;
+    ++c2;
+    used = 0;
+  }
+  // 31-bit value, like rand()
+  __device__ __forceinline__ uint32_t next() {
+    if (used == 4) refill();
+    const uint32_t r = b0;
+    b0 = b1; b1 = b2; b2 = b3;
+    ++used;
+    return r >> 1;
+  }
+};
+
+// common/constellations.c:6-28 (index = symbol value).
+template <int N>
+struct Constellation;
+template <>
+struct Constellation<1> {
+  static constexpr float pts[4] = {0.707107f, 0.707107f, -0.707107f, -0.707107f};
+};
+template <>
+struct Constellation<2> {
+  static constexpr float pts[8] = {0.707107f, 0.707107f, 0.707107f, -0.707107f,
+                                   -0.707107f, 0.707107f, -0.707107f, -0.707107f};
+};
+template <>
+struct Constellation<3> {
+  static constexpr float pts[16] = {0.408248f, 0.408248f, 0.408248f, 1.224745f,
+                                    -0.408248f, 0.408248f, -1.224745f, 0.408248f,
+                                    0.408248f, -0.408248f, 1.224745f, -0.408248f,
+                                    -0.408248f, -0.408248f, -0.408248f, -1.224745f};
+};
+
+// Encoder (common/encoder.c:84-119) one step at a time; the info bits sit in a window of up to 8
+// 32-bit words consumed MSB-first, shifted by whole words so every index is static.
+template <CodeSpec C>
+struct Encoder {
+  uint32_t w[8];
+  uint32_t state;
+  int t;
+  __device__ __forceinline__ uint32_t symbol_and_advance(int blen) {
+    const uint32_t i = t < blen ? (w[0] >> 31) : 0u;
+    const uint64_t sr = ((uint64_t)state << (64 - C.K)) | ((uint64_t)i << 63);
+    uint32_t e = 0;
+#pragma unroll
+    for (int k = 0; k < C.n; ++k) {
+      const uint64_t v = sr & C.poly[k];
+      uint32_t p = (uint32_t)__popcll(v) & 1u;
+      if (C.gen == GEN_REF_X86) p &= ((uint32_t)__popcll(v & 0x1010101010101010ull) & 1u) ^ 1u;
+      e = (e << 1) | p;
+    }
+    state = (state >> 1) | (i << (C.K - 2));
+    ++t;
+    if ((t & 31) == 0) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) w[k] = w[k + 1];
+      w[7] = 0;
+    } else {
+      w[0] <<= 1;
+    }
+    return e;
+  }
+};
+
+// Per-lane source of one block's decoder input, in decoder order. HARD: BM = Hamming distances of
+// the received symbol; soft: BM = demapped squared distances.
+template <CodeSpec C, bool HARD>
+struct ChannelSource {
+  static constexpr int NS = 1 << C.n;
+  using MT = typename std::conditional<HARD, uint32_t, float>::type;
+  Philox rng;
+  Encoder<C> enc;
+  int T, blen;
+  float scaling;
+  int32_t p_ppm;
+  void* out;       // export row of this block, or null
+
+  // Draw the info bytes (first in the stream), write them to info_out, prime the encoder.
+  __device__ __forceinline__ void init(const ChanArgs& a, int block, bool owner) {
+    T = a.r.T; blen = a.r.blen;
+    scaling = a.scaling; p_ppm = a.p_ppm;
+    rng.init(a.seed, a.first_block + (uint64_t)block);
+    const int IB = (blen + 7) >> 3;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) enc.w[k] = 0;
+    uint8_t* info = a.info_out + (size_t)block * IB;
+#pragma unroll 1
+    for (int j = 0; j < IB; ++j) {
+      const uint32_t byte = rng.next() % 256u;
+      if (owner) info[j] = (uint8_t)byte;
+      // shift the byte in at the bottom of the 256-bit register (indices stay static)
+#pragma unroll
+      for (int k = 0; k < 7; ++k) enc.w[k] = (enc.w[k] << 8) | (enc.w[k + 1] >> 24);
+      enc.w[7] = (enc.w[7] << 8) | byte;
+    }
+    // the IB bytes now sit in the low 8*IB bits of the 256-bit register w[0..7] (w[0] most
+    // significant); shift left by 256 - 8*IB bits so that info bit 0 is the MSB of w[0]
+    const int shift_words = 8 - ((IB + 3) >> 2);
+    const int shift_bytes = (4 - (IB & 3)) & 3;
+#pragma unroll 1
+    for (int s = 0; s < shift_words; ++s) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) enc.w[k] = enc.w[k + 1];
+      enc.w[7] = 0;
+    }
+    if (shift_bytes) {
+      const int sb = shift_bytes * 8;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) enc.w[k] = (enc.w[k] << sb) | (enc.w[k + 1] >> (32 - sb));
+      enc.w[7] <<= sb;
+    }
+    enc.state = 0;
+    enc.t = 0;
+    out = a.ch_out && owner
+              ? (void*)((char*)a.ch_out + (size_t)block * T * (HARD ? 1 : NS * sizeof(float)))
+              : nullptr;
+  }
+
+  __device__ __forceinline__ void next(MT (&BM)[NS]) {
+    const int t = enc.t;
+    uint32_t sym = enc.symbol_and_advance(blen);
+    if constexpr (HARD) {
+#pragma unroll
+      for (int k = 0; k < C.n; ++k)
+        if ((int32_t)(rng.next() % 1000000u) < p_ppm) sym ^= 1u << k;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) BM[k] = (uint32_t)__builtin_popcount((uint32_t)k ^ sym);
+      if (out && t < T) reinterpret_cast<uint8_t*>(out)[t] = (uint8_t)sym;
+    } else {
+      static_assert(C.n >= 1 && C.n <= 3, "the reference has constellations for n = 1..3");
+      constexpr const float* pts = Constellation<C.n>::pts;
+      float x = 0.f, y = 0.f;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        x = sym == (uint32_t)k ? pts[2 * k] : x;
+        y = sym == (uint32_t)k ? pts[2 * k + 1] : y;
+      }
+      double u1, u2;
+      do {
+        u1 = (double)rng.next() / 2147483647.0;
+        u2 = (double)rng.next() / 2147483647.0;
+      } while (u1 == 0.0);
+      const double R = sqrt(-2.0 * log(u1));
+      const double Tt = 2.0 * 3.14159265358979323846 * u2;   // 2.0 * M_PI * u2
+      double sn, cs;
+      sincos(Tt, &sn, &cs);
+      x = (float)((double)x + (double)scaling * (R * cs));
+      y = (float)((double)y + (double)scaling * (R * sn));
+      constexpr float ndx = pts[0] - pts[2], ndy = pts[1] - pts[3];
+      constexpr float nd = (ndx * ndx) + (ndy * ndy);
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const float dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
+        BM[k] = ((dx * dx) + (dy * dy)) / nd;
+      }
+      if (out && t < T) {
+        float* o = reinterpret_cast<float*>(out) + (size_t)t * NS;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) o[k] = BM[k];
+      }
+    }
+  }
+};
+
+// K <= 7: one lane per block (acs_reg.hpp), input generated in registers.
+template <CodeSpec C, bool HARD>
+__global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
+  constexpr int S = 1 << (C.K - 1);
+  constexpr int NS = 1 << C.n;
+  using DW = DecWord<S>;
+  using Src = ChannelSource<C, HARD>;
+  using MT = typename Src::MT;
+  const int b = blockIdx.x * kRegThreads + threadIdx.x;
+  const int T = a.r.T, nb = a.r.nblocks;
+  const int bc = b < nb ? b : nb - 1;
+  DW* dec = reinterpret_cast<DW*>(a.r.dec) + b;
+  const size_t dstride = (size_t)a.r.dec_stride;
+  Src src;
+  src.init(a, bc, b < nb);
+  MT M[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if constexpr (HARD) M[s] = s ? 0xFF00u : 0u;
+    else M[s] = s ? __builtin_inff() : 0.0f;
+  }
+  auto run = [&](auto sat, int t0, int t1) {
+#pragma unroll 1
+    for (int t = t0; t < t1; ++t) {
+      MT BM[NS];
+      src.next(BM);
+      dec[(size_t)t * dstride] = acs_step<C, decltype(sat)::value, MT>(M, BM);
+    }
+  };
+  // BSC saturation (reference :127-130) only matters while states are unreachable (t < K-1)
+  const int t0 = HARD ? (T < C.K - 1 ? T : C.K - 1) : 0;
+  if constexpr (HARD) run(std::true_type{}, 0, t0);
+  run(std::false_type{}, t0, T);
+  uint32_t errors = 0;
+  if (b < nb) {
+    MT best;
+    const uint32_t st = (uint32_t)argmin_state<S, MT>(M, HARD ? (MT)0xFF00u : (MT)__builtin_inff(), best);
+    if constexpr (HARD) {
+      if (a.r.path_metric) a.r.path_metric[b] = (int32_t)best;
+    }
+    errors = traceback<C.K>(a.r, b, st);
+  }
+  accumulate_errors(a.r, errors);
+}
+
+// K = 8, 9: multilane kernel (acs_multi.hpp); every lane of a block's group generates the block's
+// input (the same draws), lane q = 0 owns the info and export writes.
+template <CodeSpec C, bool HARD>
+__global__ __launch_bounds__(kRegThreads) void viterbi_channel_multi(ChanArgs a) {
+  using X = Multi<C>;
+  constexpr int NS = X::NS;
+  constexpr int n = X::n;
+  using Src = ChannelSource<C, HARD>;
+  using MT = typename Src::MT;
+  const int lane = threadIdx.x;
+  const int q = lane & (X::L - 1);
+  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  const int blk = (blockIdx.x * kRegThreads + lane) / X::L;
+  const int T = a.r.T, nb = a.r.nblocks;
+  const int bc = blk < nb ? blk : nb - 1;
+  const bool writer = q == 0 && blk < nb;
+  uint64_t* dec = reinterpret_cast<uint64_t*>(a.r.dec) + (size_t)blockIdx.x * kRegThreads + lane;
+  const size_t dstride = (size_t)a.r.dec_stride;
+  Src src;
+  src.init(a, bc, writer);
+  MT M[64];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    if constexpr (HARD) M[r] = (q == 0 && r == 0) ? 0u : 0xFF00u;
+    else M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
+  }
+  // the ring runs n steps ahead of the ACS; the source is sequential, so refills past T only draw
+  // numbers nobody uses
+  struct Step { MT v[NS]; };
+  auto load = [&](int) { Step s; src.next(s.v); return s; };
+  auto metrics = [](const Step& in, MT (&BM)[NS]) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) BM[k] = in.v[k];
+  };
+  Step ring[n];
+#pragma unroll
+  for (int k = 0; k < n; ++k) ring[k] = load(k);
+  if constexpr (HARD) {
+    multi_period<C, true, MT, 0>(0, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+    for (int t = n; t < T; t += n)
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+  } else {
+    for (int t = 0; t < T; t += n)
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+  }
+  MT best;
+  const MT sentinel = HARD ? (MT)0xFF00u : (MT)__builtin_inff();
+  const uint32_t st = multi_argmin<C, MT>(M, T % n, q, sentinel, best);
+  if constexpr (HARD) {
+    if (writer && a.r.path_metric) a.r.path_metric[blk] = (int32_t)best;
+  }
+  const uint32_t errors = multi_traceback<C>(a.r, blk, st, writer);
+  accumulate_errors(a.r, errors);
+}
+
+}  // namespace ccv

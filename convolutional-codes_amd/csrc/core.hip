@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "acs_generic.hpp"
+#include "channel_dev.hpp"
 #include "ccv.h"
 #include "reg_codes.hpp"
 #include "trellis.hpp"
@@ -69,6 +70,7 @@ struct ccv_plan {
   uint8_t* d_exp = nullptr;          // device copy of exp (generic kernel)
   DeviceBuffer dec;                  // register-kernel decision scratch
   DeviceBuffer host_in, host_out, host_pm;   // staging for ccv_decode_host
+  DeviceBuffer sim_info, sim_out;             // ccv_simulate_device scratch (caller passed none)
   hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
 };
 
@@ -242,6 +244,8 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->host_in.release();
   p->host_out.release();
   p->host_pm.release();
+  p->sim_info.release();
+  p->sim_out.release();
   if (p->d_exp) (void)hipFree(p->d_exp);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -319,6 +323,52 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     HIP_TRY(hard ? launch_generic<true>(a, *p, nblocks, stream)
                  : launch_generic<false>(a, *p, nblocks, stream));
   }
+  return 0;
+}
+
+int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t nblocks,
+                        double channel_param, uint8_t* d_info, uint8_t* d_out, int32_t* d_path_metric,
+                        unsigned long long* d_errors, void* d_channel, void* stream_v) {
+  if (!p) return fail("null plan");
+  if (!register_path(*p))
+    return fail("the on-device channel needs a register-trellis code (K <= 9 with a specialised kernel)");
+  if (p->d.channel == CCV_SOFT && p->d.n > 3)
+    return fail("no constellation for n = %d (common/constellations.c has n = 1..3)", p->d.n);
+  if (nblocks == 0) return 0;
+  if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
+  const bool hard = p->d.channel == CCV_HARD;
+  if (hard && !(channel_param >= 0.0 && channel_param <= 1000000.0))
+    return fail("BSC p_ppm must be in [0, 1e6]");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+  if (!d_info) {
+    if (p->sim_info.grow(nblocks * (size_t)p->d.info_bytes, stream)) return -1;
+    d_info = static_cast<uint8_t*>(p->sim_info.ptr);
+  }
+  if (!d_out) {
+    if (p->sim_out.grow(nblocks * (size_t)p->d.out_bytes, stream)) return -1;
+    d_out = static_cast<uint8_t*>(p->sim_out.ptr);
+  }
+  if (p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
+  ccv::ChanArgs a{};
+  a.r.in = nullptr;
+  a.r.T = p->d.steps;
+  a.r.nblocks = (int)nblocks;
+  a.r.blen = p->d.blen;
+  a.r.dec_stride = (int)padded_columns(*p, nblocks);
+  a.r.out = d_out;
+  a.r.path_metric = hard ? d_path_metric : nullptr;
+  a.r.dec = p->dec.ptr;
+  a.r.info = d_info;
+  a.r.err = d_errors;
+  a.seed = seed;
+  a.first_block = first_block;
+  a.scaling = (float)channel_param;
+  a.p_ppm = hard ? (int32_t)channel_param : 0;
+  a.info_out = d_info;
+  a.ch_out = d_channel;
+  const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
+  const bool multi = p->reg_index < 0;
+  HIP_TRY(ccv::channel_launchers(multi, hard)[multi ? p->multi_index : p->reg_index](a, grid, stream));
   return 0;
 }
 

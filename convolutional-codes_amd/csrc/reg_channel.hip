@@ -1,0 +1,48 @@
+// reg_channel.hip -- ahead-of-time instantiation of the channel-fused decode kernels
+// (channel_dev.hpp): AWGN soft and BSC hard for every register-trellis and multilane code.
+// Built with -ffp-contract=off (Makefile) so the channel's float/double arithmetic is not fused.
+#include <array>
+#include <utility>
+
+#include "channel_dev.hpp"
+#include "reg_codes.hpp"
+
+namespace ccv {
+namespace {
+
+template <size_t I, bool HARD>
+hipError_t launch_reg(const ChanArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL((viterbi_channel_reg<kRegCodes[I], HARD>), dim3(grid), dim3(kRegThreads), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+template <size_t I, bool HARD>
+hipError_t launch_multi(const ChanArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL((viterbi_channel_multi<kMultiCodes[I], HARD>), dim3(grid), dim3(kRegThreads), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+template <bool HARD, size_t... I>
+constexpr std::array<ChanLaunchFn, sizeof...(I)> make_reg(std::index_sequence<I...>) {
+  return {&launch_reg<I, HARD>...};
+}
+template <bool HARD, size_t... I>
+constexpr std::array<ChanLaunchFn, sizeof...(I)> make_multi(std::index_sequence<I...>) {
+  return {&launch_multi<I, HARD>...};
+}
+
+constexpr auto kRegSoft = make_reg<false>(std::make_index_sequence<kNumRegCodes>{});
+constexpr auto kRegHard = make_reg<true>(std::make_index_sequence<kNumRegCodes>{});
+constexpr auto kMultiSoft = make_multi<false>(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kMultiHard = make_multi<true>(std::make_index_sequence<kNumMultiCodes>{});
+
+}  // namespace
+
+const ChanLaunchFn* channel_launchers(bool multi, bool hard) {
+  if (multi) return hard ? kMultiHard.data() : kMultiSoft.data();
+  return hard ? kRegHard.data() : kRegSoft.data();
+}
+
+}  // namespace ccv

@@ -49,4 +49,9 @@ const RegLaunchFn* soft_reg_launchers(bool step_major);   // [kNumRegCodes], reg
 const RegLaunchFn* hard_reg_launchers();   // [kNumRegCodes], reg_hard.hip
 const RegLaunchFn* multi_launchers(bool hard);   // [kNumMultiCodes], reg_multi.hip
 
+struct ChanArgs;
+using ChanLaunchFn = hipError_t (*)(const ChanArgs&, int grid, hipStream_t stream);
+// channel-fused decode kernels: [kNumRegCodes] or [kNumMultiCodes], reg_channel.hip
+const ChanLaunchFn* channel_launchers(bool multi, bool hard);
+
 }  // namespace ccv

@@ -81,6 +81,21 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
                       int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
                       void* d_decisions, void* stream);
 
+/* On-device channel fused with the decode (register-trellis and multilane
+ * codes): blocks first_block .. first_block + nblocks - 1 of the Philox stream `seed` are generated in
+ * registers -- info bytes, encoder (common/encoder.c:84-119), then per step QPSK/8-PSK mapping, AWGN
+ * with noise scaling `channel_param` and the demapper (AWGN-channel/main.c:93-106, demapper.c:61-70)
+ * for a soft plan, or bit flips with probability channel_param ppm (binary-symmetric-channel/
+ * main.c:57-72) for a hard plan -- in the draw order of ccv_sim_awgn / ccv_sim_bsc(CCV_RNG_PHILOX),
+ * decoded, and the bit errors over the first blen bits of each block added to *d_errors.
+ * d_info ([nb][IB] transmitted bytes), d_out ([nb][OB] decoded bytes), d_path_metric (hard),
+ * d_errors and d_channel (export of the decoder input: float [nb][T][2^n] or uint8 [nb][T]) may be
+ * NULL; info and output then go to plan-owned scratch. Info bits and BSC symbols are bit-identical
+ * to ccv_sim_*; AWGN samples use the device's double log/sin/cos. Asynchronous on `stream`. */
+int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
+                        double channel_param, uint8_t* d_info, uint8_t* d_out, int32_t* d_path_metric,
+                        unsigned long long* d_errors, void* d_channel, void* stream);
+
 /* Synchronous convenience: host buffers in and out (staged through plan-owned device buffers). */
 int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out,
                     int32_t* path_metric);

@@ -14,6 +14,7 @@ import pytest
 import oracle_ctypes as O
 from ccviterbi import (CODEBOOK, GEN_REF_X86, GEN_TRUE_PARITY, HARD, K7, K8, K9, SOFT, Code,
                        HardDecoder, Plan, SoftDecoder, channel as ch)
+from ccviterbi import sim
 from ccviterbi.decoder import FLAG_GENERIC
 from conftest import golden_manifest
 
@@ -410,3 +411,76 @@ def test_reference_driver_with_mi355x_decoder(case, tmp_path):
         assert np.array_equal(np.fromfile(prefix + ".pm", dtype=np.int32), g["path_metric"])
     meta = dict(line.split() for line in open(prefix + ".meta"))
     assert int(meta["errors"]) == case["errors"]
+
+
+# --------------------------------------------------------------- on-device channel (ccv_simulate_device)
+
+def _simulate(torch, plan, c, seed, first, nb, param):
+    hard = plan.channel == HARD
+    d_info = torch.empty((nb, c.info_bytes), dtype=torch.uint8, device="cuda")
+    d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+    d_pm = torch.empty(nb, dtype=torch.int32, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    shape = (nb, c.steps) if hard else (nb, c.steps, 1 << c.n)
+    d_ch = torch.empty(shape, dtype=torch.uint8 if hard else torch.float32, device="cuda")
+    plan.simulate_device(seed, first, nb, param, d_errors=d_err, d_info=d_info, d_out=d_out,
+                         d_path_metric=d_pm if hard else None, d_channel=d_ch)
+    torch.cuda.synchronize()
+    return (d_info.cpu().numpy(), d_ch.cpu().numpy(), d_out.cpu().numpy(), d_pm.cpu().numpy(),
+            int(d_err.item()))
+
+
+CHANNEL_CODES = [("k7", K7), ("k7_true", K7.with_(gen_mode=GEN_TRUE_PARITY)), ("code0", CODEBOOK[0]),
+                 ("code5_r13", CODEBOOK[5]), ("k8", K8), ("k9_true", K9.with_(gen_mode=GEN_TRUE_PARITY)),
+                 ("k9_blen255", K9.with_(blen=255)), ("k7_blen1", K7.with_(blen=1))]
+
+
+@pytest.mark.parametrize("name,c", CHANNEL_CODES, ids=[x[0] for x in CHANNEL_CODES])
+def test_device_channel_bsc_bit_exact(torch_cuda, name, c):
+    """BSC frames generated on the GPU: info, received symbols, decode, path metrics and error
+    count are identical to the host Philox producer followed by the oracle decoder."""
+    for nb, first, p_ppm in ((1, 0, 100000), (200, 12345, 60000)):
+        info, syms, out, pm, err = _simulate(torch_cuda, Plan(c, HARD), c, 77, first, nb, p_ppm)
+        h_info, h_syms = ch.bsc_blocks(c, nb, p_ppm, 77, first_block=first)
+        assert np.array_equal(info, h_info)
+        assert np.array_equal(syms, h_syms)
+        ref, ref_pm = O.viterbi_hard(_ocode(c), syms)
+        assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+        assert err == ch.count_bit_errors(c, info, out)
+
+
+@pytest.mark.parametrize("name,c", CHANNEL_CODES, ids=[x[0] for x in CHANNEL_CODES])
+def test_device_channel_awgn(torch_cuda, name, c):
+    """AWGN frames generated on the GPU: info bits identical to the host Philox producer; the
+    demapped samples agree with the host's except where the device and glibc double log/sin/cos
+    round differently (tolerance below); the decode of the device's own samples is bit-exact."""
+    nb, first = 300, 999
+    scaling = ch.noise_scaling(2.0)
+    info, rx, out, _, err = _simulate(torch_cuda, Plan(c, SOFT), c, 5, first, nb, scaling)
+    h_info, h_rx = ch.awgn_blocks(c, nb, scaling, 5, first_block=first)
+    assert np.array_equal(info, h_info)
+    exact = np.mean(rx == h_rx)
+    assert exact >= 0.999, exact
+    assert np.allclose(rx, h_rx, rtol=1e-5, atol=1e-6)
+    assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
+    assert err == ch.count_bit_errors(c, info, out)
+
+
+def test_device_channel_ber_sweep_matches_host(torch_cuda):
+    """The whole-sweep driver: device-generated BSC frames give the host path's exact counts."""
+    for channel, points, c in ((HARD, [40000, 100000], K7), (SOFT, [3.0], CODEBOOK[0])):
+        kw = dict(channel=channel, bits_per_point=lambda p: 3 * 500 * c.blen, frame_blocks=500, seed=11)
+        dev = sim.ber_sweep(c, points, device_channel=True, **kw)
+        host = sim.ber_sweep(c, points, **kw)
+        for d, h in zip(dev, host):
+            assert d.bits == h.bits
+            if channel == HARD:
+                assert d.errors == h.errors
+            else:
+                assert abs(d.errors - h.errors) <= max(2, h.errors // 1000)
+
+
+def test_device_channel_rejects_generic_codes(torch_cuda):
+    plan = Plan(K9, SOFT, FLAG_GENERIC)
+    with pytest.raises(Exception, match="register-trellis"):
+        plan.simulate_device(1, 0, 10, 0.5)
