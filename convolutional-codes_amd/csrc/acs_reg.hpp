@@ -225,8 +225,9 @@ enum : int { kAblateDecStore = 1, kAblateTraceback = 2, kAblateLoads = 4 };
 
 // Soft-decision register-trellis kernel. MODE selects the input path (SoftLoad); PF is the input
 // prefetch depth in steps (per-step modes) or the steps staged per LDS round (kLoadLdsDma).
-template <CodeSpec C, int MODE, int PF, int ABLATE = 0, int NT = 0>
-__global__ __launch_bounds__(kRegThreads) void viterbi_soft_reg(RegArgs a) {
+template <CodeSpec C, int MODE, int PF, int ABLATE = 0, int NT = 0, int WAVES = 1>
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(WAVES)))
+void viterbi_soft_reg(RegArgs a) {
   constexpr int S = 1 << (C.K - 1);
   constexpr int NS = 1 << C.n;
   using DW = DecWord<S>;
@@ -275,28 +276,67 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_soft_reg(RegArgs a) {
     };
     const int sw = (lane / GRP) % UPR;
     const unsigned char* row = lds + lane * ROWB;
-    issue_chunk(0);
-    for (int t0 = 0; t0 < T; t0 += PF) {
-      float4 chunk[UPR];
+    // Decisions of a chunk are held in registers and stored right after the NEXT chunk's DMA is
+    // issued: the LDS read at a chunk start must wait for the DMA (vmcnt counts stores too, and the
+    // compiler waits for all of them), so only operations issued a whole chunk earlier may be
+    // pending there -- otherwise every chunk start drains the stores just issued.
+    DW dbuf[PF];
+    auto store_chunk = [&](int tc, bool full) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if constexpr ((ABLATE & kAblateDecStore) != 0) asm volatile("" ::"v"(dbuf[u]));
+        else if (full || tc + u < T) dec[(size_t)(tc + u) * dstride] = dbuf[u];
+      }
+    };
+    auto read_chunk = [&](float4 (&chunk)[UPR]) {
 #pragma unroll
       for (int x = 0; x < UPR; ++x) chunk[x] = *reinterpret_cast<const float4*>(row + ((x ^ sw) * 16));
+    };
+    auto acs = [&](const float4 (&chunk)[UPR], int u) {
+      SoftStep<NS> cur;
+#pragma unroll
+      for (int q = 0; q < NS / 4; ++q) {
+        const float4 v = chunk[u * (NS / 4) + q];
+        cur.v[4 * q] = v.x; cur.v[4 * q + 1] = v.y; cur.v[4 * q + 2] = v.z; cur.v[4 * q + 3] = v.w;
+      }
+      dbuf[u] = acs_step<C, false, float>(M, cur.v);
+      __builtin_amdgcn_sched_barrier(0);   // schedule step by step: interleaving steps only adds VGPRs
+    };
+    issue_chunk(0);
+    const int full_end = T / PF * PF;
+    int t0 = 0;
+    // full chunks: straight-line steps (no per-step guards for the compiler to if-convert)
+    for (; t0 < full_end; t0 += PF) {
+      float4 chunk[UPR];
+      read_chunk(chunk);
       if (t0 + PF < T) {
         // the chunk is in registers once these reads return; only then may the DMA overwrite it
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         issue_chunk(t0 + PF);                  // lands while this chunk is decoded
       }
+      if (t0 > 0) store_chunk(t0 - PF, true);
 #pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        if (t0 + u < T) {
-          SoftStep<NS> cur;
+      for (int u = 0; u < PF; ++u) acs(chunk, u);
+    }
+    if (t0 < T) {
+      // the partial last chunk: one step per iteration straight from LDS (a rolled loop -- unrolled
+      // guarded steps make the register allocator keep two copies of the metrics)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (t0 > 0) store_chunk(t0 - PF, true);
+#pragma unroll 1
+      for (int u = 0; t0 + u < T; ++u) {
+        SoftStep<NS> cur;
 #pragma unroll
-          for (int q = 0; q < NS / 4; ++q) {
-            const float4 v = chunk[u * (NS / 4) + q];
-            cur.v[4 * q] = v.x; cur.v[4 * q + 1] = v.y; cur.v[4 * q + 2] = v.z; cur.v[4 * q + 3] = v.w;
-          }
-          step(cur, t0 + u);
+        for (int q = 0; q < NS / 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(row + (((u * (NS / 4) + q) ^ sw) * 16));
+          cur.v[4 * q] = v.x; cur.v[4 * q + 1] = v.y; cur.v[4 * q + 2] = v.z; cur.v[4 * q + 3] = v.w;
         }
+        const DW d = acs_step<C, false, float>(M, cur.v);
+        if constexpr ((ABLATE & kAblateDecStore) != 0) asm volatile("" ::"v"(d));
+        else dec[(size_t)(t0 + u) * dstride] = d;
       }
+    } else {
+      store_chunk(t0 - PF, true);
     }
   } else {
     // per-lane step loads: block-major (64 distinct lines per load) or step-major (coalesced)
