@@ -29,11 +29,13 @@ HBM_PEAK_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-lev
 METRIC = "decoded Mbit/s + BER vs Eb/N0, K=7 r=1/2 soft Viterbi @1/2/4/8 MI355X"
 
 
-def algorithmic_bytes_per_bit(code, soft=True):
+def algorithmic_bytes_per_bit(code, soft=True, decisions=True):
     """B = [T*(in_step_bytes + S/8) + ceil(blen/8)] / blen bytes per info bit
-    (input stream + packed survivor decisions + decoded output)."""
+    (input stream + packed survivor decisions + decoded output). The stack decoder keeps no
+    decisions: B = [T*in_step_bytes + ceil(blen/8)] / blen."""
     step_in = (4 << code.n) if soft else 1
-    return (code.steps * (step_in + code.states / 8.0) + code.info_bytes) / code.blen
+    dec = code.states / 8.0 if decisions else 0.0
+    return (code.steps * (step_in + dec) + code.info_bytes) / code.blen
 
 
 def cpu_threads():
@@ -42,14 +44,17 @@ def cpu_threads():
     return max(1, min(16, n))
 
 
-def cpu_baseline(code, rx, gpu_out, target_cpu_seconds):
+def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, stack=False):
     """Reference decoder (oracle/_ref, compiled from the reference's own sources) on host cores,
     over a bounded sample of the SAME frames the GPU decodes; its output is checked against the GPU's.
     Falls back to the oracle restatement ("port", one thread) where oracle/_ref was not built."""
-    ref_so = os.path.join(REPO, "oracle", "_ref", "libccref_awgn.so")
+    ref_so = os.path.join(REPO, "oracle", "_ref", "libccref_awgn_stack.so" if stack else "libccref_awgn.so")
     polys = (ctypes.c_uint64 * code.n)(*code.polys)
     if os.path.exists(ref_so):
         lib = ctypes.CDLL(ref_so)
+        if stack:
+            lib.ccref_set_stack_metrics.argtypes = [ctypes.c_float, ctypes.c_int32, ctypes.c_int32]
+            lib.ccref_set_stack_metrics(code.metric_weight, *code.bit_metrics)
         lib.ccref_decode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -73,7 +78,7 @@ def cpu_baseline(code, rx, gpu_out, target_cpu_seconds):
 
         def run(nb, nthr):
             t0 = time.perf_counter()
-            out = O.viterbi_soft(oc, rx[:nb])
+            out = O.stack_soft(oc, code.metric_weight, rx[:nb]) if stack else O.viterbi_soft(oc, rx[:nb])
             return time.perf_counter() - t0, out
         kind = "port"
     t_cal, _ = run(200, 1)                      # calibrate: seconds per block on one core
@@ -82,6 +87,17 @@ def cpu_baseline(code, rx, gpu_out, target_cpu_seconds):
     nb -= nb % threads
     secs, out = run(nb, threads)
     parity = bool(np.array_equal(out, gpu_out[:nb]))
+    if stack and not parity and kind == "reference":
+        # each reference thread is a fresh decoder, while the GPU batch continues one decoder's
+        # streaming context; a stack search that overtakes the frontier reads that context, so the
+        # first block of each thread's share may legitimately differ -- compare the rest
+        per, extra = nb // threads, nb % threads
+        starts, first = set(), 0
+        for t in range(threads):
+            starts.add(first)
+            first += per + (1 if t < extra else 0)
+        diff = set(np.nonzero((out != gpu_out[:nb]).any(axis=1))[0].tolist())
+        parity = diff <= starts
     bits = nb * code.blen
     return {"value": round(bits / secs / 1e6, 4), "unit": "Mbit/s", "cores": threads, "kind": kind,
             "sample": f"{nb} blocks ({bits} info bits) of the benchmark frames, {secs:.2f} s wall on "
@@ -107,7 +123,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--code", default="k7", help="k7, k9, code0..code5 (suffix :true = true parity)")
+    ap.add_argument("--code", default=None,
+                    help="k7 (default), k9, k15 (stack default), code0..code5; suffix :true = true parity")
+    ap.add_argument("--decoder", choices=("viterbi", "stack"), default="viterbi",
+                    help="viterbi (BASELINE configs 1-4) or the stack decoder (config 5, K=15)")
     ap.add_argument("--frames", type=int, default=64,
                     help="1 M-bit frames per GPU per step (64 = 1.6 M blocks = 25,000 one-wave tiles, "
                          "~6 waves per SIMD so the last partial round is a small fraction)")
@@ -125,7 +144,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from ccviterbi import SOFT, Plan, channel as ch, named_code
+    from ccviterbi import SOFT, Plan, StackPlan, channel as ch, named_code
     from ccviterbi.decoder import FLAG_STEP_MAJOR
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -137,6 +156,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    stack = args.decoder == "stack"
+    if args.code is None:
+        args.code = "k15" if stack else "k7"
+    if stack and args.layout != "block":
+        raise SystemExit("the stack decoder reads block-major input")
     code = named_code(args.code)
     nb = args.frames * FRAME_BLOCKS
     # this rank's frames: blocks [rank*nb, (rank+1)*nb) of the Philox stream
@@ -147,7 +171,7 @@ def main():
     d_info = torch.from_numpy(info).to("cuda")
     d_out = torch.empty((nb, code.out_bytes), dtype=torch.uint8, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
-    plan = Plan(code, SOFT, FLAG_STEP_MAJOR if args.layout == "step" else 0)
+    plan = StackPlan(code, SOFT) if stack else Plan(code, SOFT, FLAG_STEP_MAJOR if args.layout == "step" else 0)
     plan.reserve(nb)
     stream = torch.cuda.current_stream()
 
@@ -194,7 +218,7 @@ def main():
     # informational: the same frames generated AND decoded on the GPU (ccv_simulate_device, the
     # on-device channel of SURVEY.md 8(f) #1) -- no host producer, no input in HBM
     fused = None
-    if rank == 0 and not args.no_fused_channel:
+    if rank == 0 and not args.no_fused_channel and not stack:
         d_ferr = torch.zeros(1, dtype=torch.int64, device="cuda")
         scaling = ch.noise_scaling(args.ebn0)
         plan.simulate_device(args.seed, 0, nb, scaling, d_errors=d_ferr, stream=stream)   # warm-up
@@ -222,14 +246,14 @@ def main():
     errors = int(errs.item())
 
     if rank == 0:
-        bpb = algorithmic_bytes_per_bit(code)
+        bpb = algorithmic_bytes_per_bit(code, decisions=not stack)
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         workload_key = f"{args.code}:frames{args.frames}:{args.layout}"
         traffic = load_pmc_traffic(workload_key)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, _ = cpu_baseline(code, rx, d_out.cpu().numpy(), args.cpu_seconds)
+            cpu, _ = cpu_baseline(code, rx, d_out.cpu().numpy(), args.cpu_seconds, stack=stack)
         line = {
             "metric": METRIC,
             "value": round(bits_per_step * args.steps / wall / 1e6, 2),
@@ -246,7 +270,8 @@ def main():
                     "resident in HBM before timing",
             "config": {
                 "workload": f"awgn-simulation {code.name or args.code} r=1/{code.n} K={code.K} soft "
-                            f"Viterbi, blen {code.blen}, {args.frames} x 1M-bit frames per GPU per step",
+                            f"{'stack decoder' if stack else 'Viterbi'}, blen {code.blen}, "
+                            f"{args.frames} x 1M-bit frames per GPU per step",
                 "code": args.code,
                 "generator": "ref-x86" if code.gen_mode == 0 else "true-parity",
                 "frames_per_gpu_per_step": args.frames,

@@ -18,6 +18,17 @@ class NativeLibraryError(RuntimeError):
     pass
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm ships its own libamdhip64 with the same SONAME (libamdhip64.so.7) as the
+    system ROCm our libraries link. Whichever loads first serves the whole process, and PyTorch sees
+    no device if the system runtime came first. Importing torch (when installed) before our
+    libraries makes its runtime the shared one; without torch the system runtime is used."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 class CcvPlanDesc(ctypes.Structure):
     """ccv_plan_desc (include/ccv.h)."""
     _fields_ = [(name, ctypes.c_int) for name in (
@@ -31,6 +42,7 @@ _cache = {}
 def _load(name):
     if name in _cache:
         return _cache[name]
+    _share_torch_hip_runtime()
     path = os.path.join(LIB_DIR, name)
     if not os.path.exists(path):
         raise NativeLibraryError(
@@ -62,6 +74,10 @@ def core():
     L.ccv_decode_device.restype = _i
     L.ccv_simulate_device.argtypes = [_vp, _u64, _u64, _sz, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp]
     L.ccv_simulate_device.restype = _i
+    L.ccv_stack_plan_create.argtypes = [_P(_vp), _i, _i, _i, _i, _P(_u64), _i, ctypes.c_float, _vp]
+    L.ccv_stack_plan_create.restype = _i
+    L.ccv_stack_decode_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.ccv_stack_decode_device.restype = _i
     L.ccv_decode_host.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.ccv_decode_host.restype = _i
     L.ccv_device_count.argtypes = []

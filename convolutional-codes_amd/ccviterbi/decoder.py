@@ -15,7 +15,7 @@ import numpy as np
 from . import _native
 from .code import GEN_REF_X86, HARD, SOFT, Code
 
-KERNEL_REGISTER, KERNEL_GENERIC, KERNEL_MULTILANE = 1, 2, 3
+KERNEL_REGISTER, KERNEL_GENERIC, KERNEL_MULTILANE, KERNEL_STACK = 1, 2, 3, 4
 FLAG_GENERIC = 1
 FLAG_STEP_MAJOR = 2
 
@@ -68,7 +68,7 @@ class Plan:
     @property
     def kernel(self):
         return {KERNEL_REGISTER: "register", KERNEL_GENERIC: "generic",
-                KERNEL_MULTILANE: "multilane"}[self.desc.kernel]
+                KERNEL_MULTILANE: "multilane", KERNEL_STACK: "stack"}[self.desc.kernel]
 
     def trellis(self) -> np.ndarray:
         out = np.zeros((self.desc.states, 2), np.uint8)
@@ -118,6 +118,37 @@ class Plan:
         if getattr(self, "_h", None):
             self._lib.ccv_plan_destroy(self._h)
             self._h = None
+
+
+class StackPlan(Plan):
+    """Stack (sequential) decoder plan (ccv_stack_plan_create): AWGN-channel/stack-decoder.c or
+    binary-symmetric-channel/stack-decoder.c, metrics from the code (code_param.metric_weight /
+    bit_metrics). decode_host / decode_device behave as one fresh decoder fed the blocks in order."""
+
+    def __init__(self, code: Code, channel: int = SOFT):
+        self.code = code
+        self.channel = channel
+        self._lib = _native.core()
+        self._polys = code.poly_array()
+        self._bm = (ctypes.c_int32 * 2)(*code.bit_metrics)
+        h = ctypes.c_void_p()
+        if self._lib.ccv_stack_plan_create(ctypes.byref(h), channel, code.n, code.K, code.blen,
+                                           self._polys, code.gen_mode, float(code.metric_weight),
+                                           self._bm) != 0:
+            raise DecoderError(f"ccv_stack_plan_create: {_native.last_error()}")
+        self._h = h
+        self.desc = _native.CcvPlanDesc()
+        self._lib.ccv_plan_describe(self._h, ctypes.byref(self.desc))
+
+    def decode_stack_device(self, d_in, nblocks, d_out, d_prev=None, d_path_metric=None, d_info=None,
+                            d_errors=None, d_status=None, stream=None):
+        """ccv_stack_decode_device: d_prev = the block the decoder saw before block 0 (None = fresh);
+        d_status[nb] flags blocks whose search would make the reference read past its buffers."""
+        rc = self._lib.ccv_stack_decode_device(self._h, _ptr(d_in), int(nblocks), _ptr(d_prev),
+                                               _ptr(d_out), _ptr(d_path_metric), _ptr(d_info),
+                                               _ptr(d_errors), _ptr(d_status), _stream_handle(stream))
+        if rc != 0:
+            raise DecoderError(f"ccv_stack_decode_device: {_native.last_error()}")
 
     def __del__(self):
         try:

@@ -1,11 +1,16 @@
 // api_shim.cpp -- reference-compatible decoder_* API over libccv_core.
 //
-// Compiled twice: -DCCV_SHIM_AWGN -> libccv_awgn.so (include/decoder_awgn.h) and
-// -DCCV_SHIM_BSC -> libccv_bsc.so (include/decoder_bsc.h). Life cycle and semantics follow
-// AWGN-channel/viterbi-decoder.c:143-236 and binary-symmetric-channel/viterbi-decoder.c:152-243:
-// streaming input, a block completes after block_len + K - 1 steps, the output callback fires
-// synchronously inside decoder_input(), a callback returning 0 takes ownership of the output buffer,
-// and the decoder resets itself after every block. Each completed block is decoded on the GPU.
+// Compiled four times: -DCCV_SHIM_AWGN -> libccv_awgn.so (include/decoder_awgn.h) and
+// -DCCV_SHIM_BSC -> libccv_bsc.so (include/decoder_bsc.h) replace the Viterbi decoders; with
+// -DCCV_SHIM_STACK added -> libccv_stack_{awgn,bsc}.so replace the stack decoders
+// (AWGN-channel/stack-decoder.c, binary-symmetric-channel/stack-decoder.c; same decoder.h). Life
+// cycle and semantics follow AWGN-channel/viterbi-decoder.c:143-236 and
+// binary-symmetric-channel/viterbi-decoder.c:152-243 (stack-decoder.c:45-197 alike): streaming
+// input, a block completes after block_len + K - 1 steps, the output callback fires synchronously
+// inside decoder_input(), a callback returning 0 takes ownership of the output buffer, and the
+// decoder resets itself after every block. Each completed block is decoded on the GPU. The stack
+// decoder's input buffer outlives a block (stack-decoder.c:105-115 does not clear it), so the
+// previous block is passed along as its streaming context (ccv_stack_decode_host).
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -40,6 +45,8 @@ struct decoder {
   uint8_t* output_data = nullptr;
   std::vector<uint8_t> batch_out;
   std::vector<int32_t> batch_pm;
+  std::vector<in_t> prev;      // stack: the last completed block (the input buffer's contents)
+  bool prev_valid = false;
 };
 
 namespace {
@@ -84,6 +91,21 @@ int decode_host(decoder* obj, const in_t* data, size_t n_blocks, uint8_t* out, i
   return 0;
 }
 
+// Blocks arriving through the streaming API: the stack decoder continues from the previous block.
+int decode_stream(decoder* obj, const in_t* data, size_t n_blocks, uint8_t* out, int32_t* pm) {
+#if defined(CCV_SHIM_STACK)
+  if (ccv_stack_decode_host(obj->plan, data, n_blocks, obj->prev_valid ? obj->prev.data() : nullptr,
+                            out, pm, nullptr) != 0)
+    return shim_fail(ccv_last_error());
+  const size_t per_block = obj->steps * obj->step_elems;
+  obj->prev.assign(data + (n_blocks - 1) * per_block, data + n_blocks * per_block);
+  obj->prev_valid = true;
+  return 0;
+#else
+  return decode_host(obj, data, n_blocks, out, pm);
+#endif
+}
+
 }  // namespace
 
 CCV_EXPORT struct decoder* decoder_create(void) {
@@ -111,9 +133,19 @@ CCV_EXPORT int decoder_init(struct decoder* obj, struct code_param* param) {
   obj->parameter = *param;   // by value; the polynomial array stays borrowed (reference :169)
   ccv_plan_destroy(obj->plan);
   obj->plan = nullptr;
+#if defined(CCV_SHIM_STACK)
+  // stack-decoder.c:74-103 reallocates its input buffer: no streaming context survives init
+  obj->prev_valid = false;
+  if (CCV_CHANNEL == CCV_HARD && param->bit_metrics == nullptr) return shim_fail("null bit_metrics");
+  if (ccv_stack_plan_create(&obj->plan, CCV_CHANNEL, param->symlen_out, param->constr_len,
+                            param->block_len, param->polynomials, obj->gen_mode, param->metric_weight,
+                            param->bit_metrics) != 0)
+    return shim_fail(ccv_last_error());
+#else
   if (ccv_plan_create(&obj->plan, CCV_CHANNEL, param->symlen_out, param->constr_len,
                       param->block_len, param->polynomials, obj->gen_mode, 0) != 0)
     return shim_fail(ccv_last_error());
+#endif
   ccv_plan_desc d;
   ccv_plan_describe(obj->plan, &d);
   obj->steps = (size_t)d.steps;
@@ -137,8 +169,8 @@ static int receive_step(decoder* obj, const in_t* step) {
               obj->step_elems * sizeof(in_t));
   if (++obj->symbol_counter < obj->steps) return 0;
   int32_t pm = 0;
-  if (decode_host(obj, obj->block.data(), 1, obj->output_data,
-                  CCV_CHANNEL == CCV_HARD ? &pm : nullptr) != 0)
+  if (decode_stream(obj, obj->block.data(), 1, obj->output_data,
+                    CCV_CHANNEL == CCV_HARD ? &pm : nullptr) != 0)
     return -1;
   if (emit_output_buffer(obj, pm) != 0) return -1;
   decoder_reset(obj);
@@ -182,8 +214,8 @@ CCV_EXPORT int decoder_input_blocks(struct decoder* obj, const in_t* data, size_
     const size_t nb = n_blocks - first < kBatchChunk ? n_blocks - first : kBatchChunk;
     obj->batch_out.resize(nb * obj->out_bytes);
     obj->batch_pm.resize(nb);
-    if (decode_host(obj, data + first * per_block, nb, obj->batch_out.data(),
-                    CCV_CHANNEL == CCV_HARD ? obj->batch_pm.data() : nullptr) != 0)
+    if (decode_stream(obj, data + first * per_block, nb, obj->batch_out.data(),
+                      CCV_CHANNEL == CCV_HARD ? obj->batch_pm.data() : nullptr) != 0)
       return -1;
     for (size_t b = 0; b < nb; ++b) {
       std::memcpy(obj->output_data, &obj->batch_out[b * obj->out_bytes], obj->out_bytes);

@@ -9,9 +9,14 @@
 
 #include "acs_generic.hpp"
 #include "channel_dev.hpp"
+#include "stack_dev.hpp"
 #include "ccv.h"
 #include "reg_codes.hpp"
 #include "trellis.hpp"
+
+namespace ccv {
+hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s);   // stack.hip
+}
 
 namespace {
 
@@ -64,6 +69,9 @@ struct ccv_plan {
   std::vector<uint8_t> exp;          // [S][2]
   int reg_index = -1;                // kRegCodes index, or -1
   int multi_index = -1;              // kMultiCodes index (K = 8, 9), or -1
+  bool stack = false;                // stack (sequential) decoder plan
+  float metric_weight = 0.0f;        // stack, soft: code_param.metric_weight
+  int32_t bit_metrics[2] = {0, 0};   // stack, hard: code_param.bit_metrics
   bool step_major = false;           // soft input layout [T][nblocks][2^n] (CCV_FLAG_STEP_MAJOR)
   int generic_spt = 1, generic_threads = 64, generic_chunk = 1;
   size_t generic_lds = 0;
@@ -278,6 +286,11 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
   if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
   hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
   const bool hard = p->d.channel == CCV_HARD;
+  if (p->stack) {
+    if (d_decisions) return fail("a stack decoder has no survivor decisions");
+    return ccv_stack_decode_device(p, d_in, nblocks, nullptr, d_out, d_path_metric, d_info, d_errors,
+                                   nullptr, stream_v);
+  }
   if (register_path(*p)) {
     if (d_decisions && p->reg_index < 0)
       return fail("decision export needs the single-lane register kernel (K <= 7)");
@@ -326,10 +339,95 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
   return 0;
 }
 
+int ccv_stack_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const uint64_t* polys,
+                          int gen_mode, float metric_weight, const int32_t* bit_metrics) {
+  if (!out) return fail("ccv_stack_plan_create: null output pointer");
+  *out = nullptr;
+  if (channel != CCV_SOFT && channel != CCV_HARD) return fail("bad channel %d", channel);
+  if (n < 1 || n > ccv::kMaxN) return fail("n=%d unsupported (1..%d)", n, ccv::kMaxN);
+  if (K < 2 || K > 64) return fail("K=%d unsupported (2..64, stack-decoder.c keeps a uint64_t state)", K);
+  if (blen < 1 || blen > 255) return fail("blen=%d unsupported (1..255)", blen);
+  if (!polys) return fail("null polynomials");
+  if (gen_mode != CCV_GEN_REF_X86 && gen_mode != CCV_GEN_TRUE_PARITY)
+    return fail("bad generator mode %d", gen_mode);
+  const int T = blen + K - 1;
+  if (channel == CCV_HARD && T > 255)
+    return fail("T=%d > 255: the BSC stack decoder's uint8_t indices wrap", T);
+  if (channel == CCV_HARD && !bit_metrics) return fail("null bit metrics");
+  if (channel == CCV_SOFT && ((size_t)T << n) > 65535)
+    return fail("T * 2^n = %zu floats: the AWGN stack decoder's uint16_t index wraps", (size_t)T << n);
+  if (channel == CCV_SOFT && 2 * ((size_t)T << n) * sizeof(float) > 64 * 1024)
+    return fail("T * 2^n too large for the staged input (64 KiB of LDS)");
+  ccv_plan* p = new ccv_plan();
+  p->stack = true;
+  p->metric_weight = metric_weight;
+  if (bit_metrics) {
+    p->bit_metrics[0] = bit_metrics[0];
+    p->bit_metrics[1] = bit_metrics[1];
+  }
+  p->d.channel = channel;
+  p->d.n = n;
+  p->d.K = K;
+  p->d.blen = blen;
+  p->d.gen_mode = gen_mode;
+  p->d.steps = T;
+  p->d.states = 0;   // no trellis: the search keeps at most 64 paths
+  p->d.info_bytes = (blen + 7) / 8;
+  p->d.out_bytes = (T + 7) / 8;
+  p->d.in_step_bytes = channel == CCV_SOFT ? (int)sizeof(float) << n : 1;
+  p->d.kernel = CCV_KERNEL_STACK;
+  p->d.lanes = ccv::kStackDepth;
+  memcpy(p->polys, polys, sizeof(uint64_t) * (size_t)n);
+  hipError_t e = hipGetDevice(&p->d.device);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    delete p;
+    return fail("no HIP device: %s", hipGetErrorString(e));
+  }
+  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    delete p;
+    return fail("hipStreamCreate failed");
+  }
+  *out = p;
+  return 0;
+}
+
+int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const void* d_prev,
+                            uint8_t* d_out, int32_t* d_path_metric, const uint8_t* d_info,
+                            unsigned long long* d_errors, int32_t* d_status, void* stream_v) {
+  if (!p) return fail("null plan");
+  if (!p->stack) return fail("not a stack-decoder plan (ccv_stack_plan_create)");
+  if (nblocks == 0) return 0;
+  if (!d_in || !d_out) return fail("null device buffer");
+  if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
+  ccv::StackArgs a{};
+  a.in = d_in;
+  a.prev = d_prev;
+  a.n = p->d.n;
+  a.K = p->d.K;
+  a.T = p->d.steps;
+  a.blen = p->d.blen;
+  a.gen = p->d.gen_mode;
+  memcpy(a.poly, p->polys, sizeof a.poly);
+  a.weight = p->metric_weight;
+  a.bm0 = p->bit_metrics[0];
+  a.bm1 = p->bit_metrics[1];
+  a.nblocks = (int)nblocks;
+  a.out = d_out;
+  a.path_metric = p->d.channel == CCV_HARD ? d_path_metric : nullptr;
+  a.info = d_info;
+  a.err = d_info ? d_errors : nullptr;
+  a.status = d_status;
+  HIP_TRY(ccv::launch_stack(a, p->d.channel == CCV_HARD, reinterpret_cast<hipStream_t>(stream_v)));
+  return 0;
+}
+
 int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, uint8_t* d_info, uint8_t* d_out, int32_t* d_path_metric,
                         unsigned long long* d_errors, void* d_channel, void* stream_v) {
   if (!p) return fail("null plan");
+  if (p->stack) return fail("the on-device channel is implemented for the Viterbi kernels");
   if (!register_path(*p))
     return fail("the on-device channel needs a register-trellis code (K <= 9 with a specialised kernel)");
   if (p->d.channel == CCV_SOFT && p->d.n > 3)
@@ -369,6 +467,37 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
   const bool multi = p->reg_index < 0;
   HIP_TRY(ccv::channel_launchers(multi, hard)[multi ? p->multi_index : p->reg_index](a, grid, stream));
+  return 0;
+}
+
+int ccv_stack_decode_host(ccv_plan* p, const void* in, size_t nblocks, const void* prev, uint8_t* out,
+                          int32_t* path_metric, int32_t* status) {
+  if (!p) return fail("null plan");
+  if (!p->stack) return fail("not a stack-decoder plan (ccv_stack_plan_create)");
+  if (nblocks == 0) return 0;
+  if (!in || !out) return fail("null host buffer");
+  const size_t block_bytes = (size_t)p->d.steps * (size_t)p->d.in_step_bytes;
+  const size_t in_bytes = (nblocks + 1) * block_bytes;   // slot 0: the previous block
+  const size_t out_bytes = nblocks * (size_t)p->d.out_bytes;
+  const size_t aux_bytes = 2 * nblocks * sizeof(int32_t);   // path metrics, status
+  if (p->host_in.grow(in_bytes, p->stream) || p->host_out.grow(out_bytes, p->stream) ||
+      p->host_pm.grow(aux_bytes, p->stream))
+    return -1;
+  unsigned char* d_in = static_cast<unsigned char*>(p->host_in.ptr);
+  int32_t* d_pm = static_cast<int32_t*>(p->host_pm.ptr);
+  if (prev) HIP_TRY(hipMemcpyAsync(d_in, prev, block_bytes, hipMemcpyHostToDevice, p->stream));
+  HIP_TRY(hipMemcpyAsync(d_in + block_bytes, in, nblocks * block_bytes, hipMemcpyHostToDevice, p->stream));
+  if (ccv_stack_decode_device(p, d_in + block_bytes, nblocks, prev ? d_in : nullptr,
+                              static_cast<uint8_t*>(p->host_out.ptr), d_pm, nullptr, nullptr,
+                              d_pm + nblocks, p->stream))
+    return -1;
+  HIP_TRY(hipMemcpyAsync(out, p->host_out.ptr, out_bytes, hipMemcpyDeviceToHost, p->stream));
+  if (path_metric && p->d.channel == CCV_HARD)
+    HIP_TRY(hipMemcpyAsync(path_metric, d_pm, nblocks * sizeof(int32_t), hipMemcpyDeviceToHost, p->stream));
+  if (status)
+    HIP_TRY(hipMemcpyAsync(status, d_pm + nblocks, nblocks * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           p->stream));
+  HIP_TRY(hipStreamSynchronize(p->stream));
   return 0;
 }
 

@@ -27,26 +27,36 @@ const float kConst3[] = {0.408248f, 0.408248f, 0.408248f, 1.224745f,
 const float* constellation(int n) { return n == 1 ? kConst1 : n == 2 ? kConst2 : n == 3 ? kConst3 : nullptr; }
 
 struct Code {
-  int n, K, blen, T, IB, S;
-  std::vector<uint8_t> exp;
-  bool init(int n_, int K_, int blen_, const uint64_t* polys, int gen) {
-    if (n_ < 1 || n_ > ccv::kMaxN || K_ < 2 || K_ > ccv::kMaxK || blen_ < 1 || blen_ > 255 || !polys)
+  int n, K, blen, T, IB, gen;
+  uint64_t poly[ccv::kMaxN];
+  std::vector<uint8_t> exp;   // trellis table for K <= kMaxK; longer codes (stack decoder) compute
+  bool init(int n_, int K_, int blen_, const uint64_t* polys, int gen_) {
+    if (n_ < 1 || n_ > ccv::kMaxN || K_ < 2 || K_ > 64 || blen_ < 1 || blen_ > 255 || !polys)
       return false;
-    n = n_; K = K_; blen = blen_;
+    n = n_; K = K_; blen = blen_; gen = gen_;
     T = blen + K - 1;
     IB = (blen + 7) / 8;
-    S = 1 << (K - 1);
-    exp.resize(2 * (size_t)S);
-    ccv::build_trellis(n, K, polys, gen, exp.data());
+    std::memcpy(poly, polys, sizeof(uint64_t) * (size_t)n);
+    if (K <= ccv::kMaxK) {
+      exp.resize(size_t{2} << (K - 1));
+      ccv::build_trellis(n, K, polys, gen, exp.data());
+    }
     return true;
   }
   // common/encoder.c:84-119: the encoder's shift register after shifting in bit i is exactly the
   // decoder's (state << (64-K)) | (i << 63) with state = the previous K-1 inputs.
   void encode(const uint8_t* info, uint8_t* syms) const {
-    uint32_t s = 0;
+    uint64_t s = 0;
     for (int t = 0; t < T; ++t) {
-      uint32_t i = t < blen ? (info[t / 8] >> (7 - t % 8)) & 1u : 0u;
-      syms[t] = exp[2 * s + i];
+      uint64_t i = t < blen ? (info[t / 8] >> (7 - t % 8)) & 1u : 0u;
+      if (!exp.empty()) {
+        syms[t] = exp[2 * s + i];
+      } else {
+        const uint64_t sr = (s << (64 - K)) | (i << 63);
+        int e = 0;
+        for (int k = 0; k < n; ++k) e = (e << 1) | ccv::gen_bit(sr & poly[k], gen);
+        syms[t] = (uint8_t)e;
+      }
       s = (s >> 1) | (i << (K - 2));
     }
   }

@@ -1,0 +1,39 @@
+// stack.hip -- launches of the wave-per-block stack decoder (stack_dev.hpp). Built with
+// -ffp-contract=off: the branch metric's float product and double sum must not fuse.
+#include "stack_dev.hpp"
+
+namespace ccv {
+
+template <bool HARD, int PW, int NP, bool W32>
+static hipError_t launch_v(const StackArgs& a, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((stack_decode<HARD, PW, NP, W32>), dim3(a.nblocks), dim3(kStackDepth), lds, s, a);
+  return hipGetLastError();
+}
+
+// rate 1/2 and 1/3 codes with K <= 32 (the codebook, K=15) get specialised symbol code
+template <bool HARD, int PW>
+static hipError_t launch_pw(const StackArgs& a, size_t lds, hipStream_t s) {
+  if (a.K <= 32) {
+    if (a.n == 2) return launch_v<HARD, PW, 2, true>(a, lds, s);
+    if (a.n == 3) return launch_v<HARD, PW, 3, true>(a, lds, s);
+  }
+  return launch_v<HARD, PW, 0, false>(a, lds, s);
+}
+
+hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
+  const size_t per = (size_t)a.T * (hard ? 1 : ((size_t)1 << a.n));
+  const size_t lds = 2 * per * (hard ? 1 : sizeof(float));
+  const int pw = (a.T + 31) / 32;
+  if (hard) {
+    if (pw <= 2) return launch_pw<true, 2>(a, lds, s);
+    if (pw <= 4) return launch_pw<true, 4>(a, lds, s);
+    if (pw <= 8) return launch_pw<true, 8>(a, lds, s);
+    return launch_pw<true, 10>(a, lds, s);
+  }
+  if (pw <= 2) return launch_pw<false, 2>(a, lds, s);
+  if (pw <= 4) return launch_pw<false, 4>(a, lds, s);
+  if (pw <= 8) return launch_pw<false, 8>(a, lds, s);
+  return launch_pw<false, 10>(a, lds, s);
+}
+
+}  // namespace ccv

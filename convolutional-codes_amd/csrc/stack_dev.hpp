@@ -1,0 +1,267 @@
+// stack_dev.hpp -- the reference's stack (sequential) decoder on CDNA4, one wave per block.
+//
+// Reference: AWGN-channel/stack-decoder.c and binary-symmetric-channel/stack-decoder.c. A block is
+// decoded by repeatedly extending the most probable path of a 64-entry path stack (STACK_DEPTH,
+// :12) by both inputs until it spans the received frontier (:132-197); when the stack is full the
+// least probable path is overwritten (duplicate_path, :227-241).
+//
+// MI355X mapping: the stack depth equals the wave width, so lane i of the wave IS stack entry i --
+// its next-input index, encoder state, metric and decoded-path bits live in that lane's VGPRs. The
+// reference's linear scans become wave reductions (row DPP + 4 readlanes) and a ballot + find-first
+// for the lowest index among equal metrics (strict > / < from -inf / +inf, :199-225); the per-
+// iteration bookkeeping is wave-uniform scalar code. There is no divergence at all: the whole wave
+// follows one block's search. The block's received symbols (and the previous block's, see below)
+// are staged once in LDS.
+//
+// Exactness: same float arithmetic as the reference -- the branch metric is
+// (float)(1.0 + (double)(weight * d[sym])) (:274, float product, double sum) and path metrics
+// accumulate in fp32 -- and the reference's streaming loop is kept: after step t arrives the most
+// probable path is extended until it ends exactly at the frontier. That matters when the stack fills
+// with equal metrics (idiom codes emit one symbol for both inputs): then the most and the least
+// probable path are the same entry, duplicate_path copies it onto itself and both extensions land on
+// it, so it skips a symbol and runs ahead of the frontier, where the reference's input buffer still
+// holds the PREVIOUS block's symbols. The kernel reads exactly that: block b-1 of the batch (block 0:
+// the caller's previous block, or zeros for a fresh decoder). A search that would read past the
+// buffer (the reference then reads unrelated heap memory) is reported in the per-block status.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "trellis.hpp"
+
+namespace ccv {
+
+struct StackArgs {
+  const void* in;          // soft: float [nb][T][2^n]; hard: uint8 [nb][T]
+  const void* prev;        // the block decoded before block 0 (same layout, one block), or null
+  int n, K, T, blen, gen;
+  uint64_t poly[kMaxN];
+  float weight;            // soft: code_param.metric_weight (code.h:16)
+  int32_t bm0, bm1;        // hard: code_param.bit_metrics[0..1] (code.h:14)
+  int nblocks;
+  uint8_t* out;            // [nb][OB]
+  int32_t* path_metric;    // hard: final path metric, may be null
+  const uint8_t* info;     // optional [nb][IB]: count bit errors
+  unsigned long long* err;
+  int32_t* status;         // optional [nb]: 0 ok, 1 = the reference would read past its buffers
+};
+
+constexpr int kStackDepth = 64;   // stack-decoder.c:12 == wave64
+
+// Wave-wide max / min, result in every lane's register and returned as a uniform value. Row-level
+// butterflies, then row_bcast:15 / row_bcast:31 carry rows 0-2 upward so lane 63 holds the result.
+// Inline asm (explicit s_nop for the VALU-write -> DPP-read hazard): the compiler would wrap each
+// step in canonicalising v_max x,x and a v_mov of the DPP "old" operand. Non-finite inputs: IEEE
+// max/min skip NaN, as the reference's strict compares do.
+#define CCV_DPP_STEP(op, ctrl) "s_nop 1\n" op "_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf\n"
+#define CCV_WAVE_REDUCE(op)                                                                      \
+  CCV_DPP_STEP(op, "quad_perm:[1,0,3,2]") CCV_DPP_STEP(op, "quad_perm:[2,3,0,1]")                \
+  CCV_DPP_STEP(op, "row_half_mirror") CCV_DPP_STEP(op, "row_mirror")                              \
+  "s_nop 1\n" op "_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"                     \
+  "s_nop 1\n" op "_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+__device__ __forceinline__ float wave_max(float v) {
+  asm volatile(CCV_WAVE_REDUCE("v_max_f32") : "+v"(v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_min(float v) {
+  asm volatile(CCV_WAVE_REDUCE("v_min_f32") : "+v"(v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+  asm volatile(CCV_WAVE_REDUCE("v_max_i32") : "+v"(v));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int32_t wave_min(int32_t v) {
+  asm volatile(CCV_WAVE_REDUCE("v_min_i32") : "+v"(v));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+#undef CCV_WAVE_REDUCE
+#undef CCV_DPP_STEP
+
+__device__ __forceinline__ uint32_t bcast(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ float bcast(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ int32_t bcast(int32_t v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+// get_transition_metric's expected symbols (stack-decoder.c:249-272) for both inputs of a state,
+// packed (e0 << 8) | e1. The register (state << (64-K)) | (input << 63) differs between the inputs
+// only in bit 63, which the idiom's mask 0x1010..10 does not cover, so per polynomial one parity p
+// and one masked parity q serve both: bit(in) = (p ^ (in & poly bit 63)) & (idiom ? !q : 1).
+// Evaluated per lane in VALU for the lane's own entry (the scalar unit, shared by the CU's four
+// SIMDs, is the stack search's bottleneck). NP = n when specialised (0: runtime n); W32: K <= 32,
+// so the register lives in the upper 32 bits.
+template <int NP, bool W32>
+__device__ __forceinline__ uint32_t lane_symbols(const uint64_t (&poly)[kMaxN], int n, int K, bool idiom,
+                                                 uint64_t state) {
+  const uint64_t sr = state << (64 - K);
+  uint32_t e0 = 0, e1 = 0;
+#pragma unroll
+  for (int k = 0; k < (NP ? NP : kMaxN); ++k) {
+    if (NP || k < n) {
+      uint32_t par, q;
+      if constexpr (W32) {
+        const uint32_t v = (uint32_t)(sr >> 32) & (uint32_t)(poly[k] >> 32);
+        par = (uint32_t)__builtin_popcount(v);
+        q = (uint32_t)__builtin_popcount(v & 0x10101010u);
+      } else {
+        const uint64_t v = sr & poly[k];
+        par = (uint32_t)__popcll(v);
+        q = (uint32_t)__popcll(v & 0x1010101010101010ull);
+      }
+      const uint32_t keep = idiom ? (~q & 1u) : 1u;
+      const uint32_t b0 = par & keep;
+      const uint32_t b1 = (par ^ (uint32_t)(poly[k] >> 63)) & keep;
+      e0 = (e0 << 1) | (b0 & 1u);
+      e1 = (e1 << 1) | (b1 & 1u);
+    }
+  }
+  return (e0 << 8) | e1;
+}
+
+// PW = 32-bit words of decoded path per entry (T <= 32 * PW). Word w holds path bits 32w..32w+31,
+// first bit in the MSB, i.e. output bytes 4w..4w+3 big-endian.
+template <bool HARD, int PW, int NP, bool W32>
+__global__ __launch_bounds__(kStackDepth) void stack_decode(StackArgs a) {
+  using MT = typename std::conditional<HARD, int32_t, float>::type;
+  using ET = typename std::conditional<HARD, uint8_t, float>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x;
+  const int T = a.T;
+  const int NS = HARD ? 1 : (1 << a.n);
+  const int per = T * NS;
+  ET* cur_in = reinterpret_cast<ET*>(smem);
+  ET* prev_in = cur_in + per;
+  const ET* in = reinterpret_cast<const ET*>(a.in);
+  const ET* prev = b > 0 ? in + (size_t)(b - 1) * per : reinterpret_cast<const ET*>(a.prev);
+  for (int i = lane; i < per; i += kStackDepth) {
+    ET v = in[(size_t)b * per + i];
+    ET pv = prev ? prev[i] : (ET)0;
+    if constexpr (HARD) {   // binary-symmetric-channel/stack-decoder.c:116-118 masks each symbol
+      v = (ET)(v & ((1u << a.n) - 1u));
+      pv = (ET)(pv & ((1u << a.n) - 1u));
+    }
+    cur_in[i] = v;
+    prev_in[i] = pv;
+  }
+  __syncthreads();
+
+  // stack entry = this lane
+  uint32_t nxt = 0;      // next_input_index in trellis steps
+  uint64_t st = 0;       // encoder_state
+  MT met = 0;            // metric
+  uint32_t path[PW];
+#pragma unroll
+  for (int w = 0; w < PW; ++w) path[w] = 0;
+  int size = 1;          // next_stack_idx
+  int cur = 0;
+  int status = 0;
+  uint64_t poly[kMaxN];
+#pragma unroll
+  for (int k = 0; k < kMaxN; ++k) poly[k] = a.poly[k];
+  const int n = a.n, K = a.K;
+  const bool idiom = a.gen == GEN_REF_X86;
+  uint32_t esym = lane_symbols<NP, W32>(poly, n, K, idiom, 0);   // this entry's next symbols
+  const MT lo_sent = HARD ? (MT)INT32_MIN : (MT)-__builtin_inff();
+  const MT hi_sent = HARD ? (MT)INT32_MAX : (MT)__builtin_inff();
+
+  for (int t = 1; t <= T && !status; ++t) {
+    for (;;) {
+      // get_most_probable_path (:213-225): strict > from the lowest value, first index wins
+      const bool live = lane < size;
+      const MT mx = wave_max(live ? met : lo_sent);
+      const uint64_t hit = __ballot(live && met == mx && mx > lo_sent);
+      if (hit == 0) { status = 1; break; }
+      cur = __builtin_ctzll(hit);
+      const uint32_t c_next = bcast(nxt, cur);
+      if (c_next == (uint32_t)t) break;                 // the path ends at the frontier
+      if (c_next >= (uint32_t)T) { status = 1; break; } // would read past the input buffer
+      const uint64_t c_st = ((uint64_t)bcast((uint32_t)(st >> 32), cur) << 32) | bcast((uint32_t)st, cur);
+      const MT c_met = bcast(met, cur);
+      const uint32_t c_e = bcast(esym, cur);
+      const uint32_t e0 = c_e >> 8, e1 = c_e & 0xFFu;
+      const uint64_t ns0 = c_st >> 1;                          // successors (stack-decoder.c:272)
+      const uint64_t ns1 = ns0 | ((uint64_t)1 << (K - 2));
+      // symbols at or beyond the frontier are still the previous block's (see header)
+      const ET* row = (c_next < (uint32_t)t ? cur_in : prev_in) + (size_t)c_next * NS;
+      MT tm0, tm1;
+      if constexpr (HARD) {
+        const int32_t d0 = __builtin_popcount(e0 ^ row[0]), d1 = __builtin_popcount(e1 ^ row[0]);
+        tm0 = d0 * a.bm1 + (n - d0) * a.bm0;   // binary-symmetric-channel/stack-decoder.c:266-272
+        tm1 = d1 * a.bm1 + (n - d1) * a.bm0;
+      } else {
+        tm0 = (float)(1.0 + (double)(a.weight * row[e0]));   // AWGN-channel/stack-decoder.c:274
+        tm1 = (float)(1.0 + (double)(a.weight * row[e1]));
+      }
+      // duplicate_path (:227-241)
+      int lhs;
+      if (size == kStackDepth) {
+        const MT mn = wave_min(met);
+        const uint64_t low = __ballot(met == mn && mn < hi_sent);
+        if (low == 0) { status = 1; break; }
+        lhs = __builtin_ctzll(low);
+      } else {
+        lhs = size++;
+      }
+      // extend the current path by input 0 and the duplicate by input 1 (:154-167); when lhs == cur
+      // both extensions apply to the same entry, one after the other
+      const uint32_t n0 = c_next + 1;
+      const MT m0 = c_met + tm0;
+      const bool same = lhs == cur;
+      const uint32_t bn = same ? n0 : c_next;
+      const uint64_t bs = same ? ns0 : c_st;
+      const MT bm = same ? m0 : c_met;
+      const uint32_t w1 = bn & 0xFF;                     // outbuf_widx is uint8_t
+      if (lane == cur) { nxt = n0; st = ns0; met = m0; }
+      // lhs: copy of the current path (before its extension unless it IS the current path)
+      uint32_t cp[PW];
+#pragma unroll
+      for (int w = 0; w < PW; ++w) cp[w] = bcast(path[w], cur);
+      if (lane == lhs) {
+        nxt = bn + 1;
+        st = ns1;
+        met = bm + tm1;
+#pragma unroll
+        for (int w = 0; w < PW; ++w)
+          path[w] = cp[w] | ((uint32_t)(w1 >> 5) == (uint32_t)w ? (0x80000000u >> (w1 & 31)) : 0u);
+      }
+      (void)bs;
+      if (lane == cur || lane == lhs) esym = lane_symbols<NP, W32>(poly, n, K, idiom, st);
+    }
+  }
+  // the most probable path at the end (or entry 0 if the search stopped)
+  uint32_t res[PW];
+#pragma unroll
+  for (int w = 0; w < PW; ++w) res[w] = bcast(path[w], status ? 0 : cur);
+  const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+  uint32_t errors = 0;
+  if (lane < OB) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int w = 0; w < PW; ++w) word = (lane >> 2) == w ? res[w] : word;
+    const uint32_t byte = (word >> (24 - 8 * (lane & 3))) & 0xFFu;
+    a.out[(size_t)b * OB + lane] = (uint8_t)byte;
+    if (a.info && lane < IB) {
+      int valid = a.blen - 8 * lane;
+      valid = valid > 8 ? 8 : valid;
+      const uint32_t mask = (0xFFu << (8 - valid)) & 0xFFu;
+      errors = __builtin_popcount((byte ^ a.info[(size_t)b * IB + lane]) & mask);
+    }
+  }
+  if constexpr (HARD) {
+    if (lane == 0 && a.path_metric) a.path_metric[b] = bcast(met, status ? 0 : cur);
+  }
+  if (lane == 0 && a.status) a.status[b] = status;
+  if (a.err) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) errors += __shfl_xor(errors, off, 64);
+    if (lane == 0 && errors) atomicAdd(a.err, (unsigned long long)errors);
+  }
+}
+
+}  // namespace ccv

@@ -42,6 +42,7 @@ extern "C" {
 #define CCV_KERNEL_REGISTER 1 /* code-specialised register-trellis kernel                       */
 #define CCV_KERNEL_GENERIC 2  /* table-driven LDS kernel                                        */
 #define CCV_KERNEL_MULTILANE 3 /* K = 8, 9: register-trellis kernel, 2^(K-7) lanes per block      */
+#define CCV_KERNEL_STACK 4    /* stack (sequential) decoder, one wave per block                  */
 
 typedef struct ccv_plan ccv_plan;
 
@@ -95,6 +96,25 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
 int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, uint8_t* d_info, uint8_t* d_out, int32_t* d_path_metric,
                         unsigned long long* d_errors, void* d_channel, void* stream);
+
+/* Stack (sequential) decoder plan (AWGN-channel/stack-decoder.c, binary-symmetric-channel/
+ * stack-decoder.c): 64-entry path stack, K <= 64. metric_weight = code_param.metric_weight (soft),
+ * bit_metrics = code_param.bit_metrics[2] (hard; code.h:14-16). ccv_decode_device / ccv_decode_host
+ * accept the plan (a batch is decoded as if its blocks went through one fresh decoder in order). */
+int ccv_stack_plan_create(ccv_plan** plan, int channel, int n, int K, int blen, const uint64_t* polys,
+                          int gen_mode, float metric_weight, const int32_t* bit_metrics);
+
+/* Stack decode with the streaming context made explicit: d_prev = the block the same decoder
+ * received before block 0 (its input buffer still holds it; NULL = a fresh, zeroed decoder); blocks
+ * b > 0 follow block b-1. d_status[nb] (optional): 1 where the reference would have read past its
+ * buffers (a degenerate search; the output of that block is then not the reference's). */
+int ccv_stack_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, const void* d_prev,
+                            uint8_t* d_out, int32_t* d_path_metric, const uint8_t* d_info,
+                            unsigned long long* d_errors, int32_t* d_status, void* stream);
+
+/* Host-buffer form of ccv_stack_decode_device (prev, path_metric, status may be NULL). */
+int ccv_stack_decode_host(ccv_plan* plan, const void* in, size_t nblocks, const void* prev,
+                          uint8_t* out, int32_t* path_metric, int32_t* status);
 
 /* Synchronous convenience: host buffers in and out (staged through plan-owned device buffers). */
 int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out,

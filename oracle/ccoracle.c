@@ -278,6 +278,133 @@ void cco_viterbi_hard(const cco_code* c, const uint8_t* syms, size_t nblocks, ui
     free(exp_sym); free(M); free(N); free(prev); free(inp);
 }
 
+/* ---------------------------------------------------------------- stack decoders */
+
+/* AWGN-channel/stack-decoder.c:243-276 / binary-symmetric-channel/stack-decoder.c:235-273: the
+ * generator register is (state << (64-K)) | (input << 63) with a 64-bit state (K <= 64). */
+static int stack_symbol(const cco_code* c, uint64_t state, int input, uint64_t* new_state) {
+    uint64_t sr = (state << (64 - c->K)) | ((uint64_t)input << 63);
+    int e = 0;
+    for (int k = 0; k < c->n; ++k) e = (e << 1) | cco_gen_bit(sr & c->poly[k], c->gen_mode);
+    *new_state = sr >> (64 + 1 - c->K);
+    return e;
+}
+
+#define CCO_STACK_DEPTH 64   /* stack-decoder.c:12 */
+
+typedef struct {
+    uint16_t next;        /* next_input_index: floats (AWGN) or symbols (BSC, uint8 there) */
+    uint64_t state;
+    float fmetric;
+    int32_t imetric;
+    uint8_t path[40];
+} cco_path;
+
+/* One block with the reference's data structure and streaming loop (stack-decoder.c:105-115 reset,
+ * :132-197 receive_symbol, :199-241 most/least probable and duplicate). The loop is the streaming
+ * one: after step t arrives, extend the most probable path until it ends exactly at the received
+ * frontier. This matters when the stack is full of equal metrics (idiom codes emit the same symbol
+ * for both inputs, so twin paths accumulate): then the most and least probable path are the same
+ * entry, duplicate_path copies it onto itself and the two extensions land on one path, which skips a
+ * symbol and runs ahead of the frontier, reading whatever the input buffer holds there -- the
+ * previous block's symbols (`buf` persists across blocks like the reference's input_symbols, zeroed
+ * at creation). Returns -1 if the reference would read past its input buffer (not reproducible). */
+static int stack_block(const cco_code* c, int soft, float weight, const int32_t* bm,
+                       const float* rx, const uint8_t* syms, float* fbuf, uint8_t* hbuf,
+                       uint8_t* out, int32_t* pm) {
+    const size_t T = cco_steps(c), OB = cco_out_bytes(c);
+    const unsigned NS = soft ? (1u << c->n) : 1u;
+    const uint8_t mask = (uint8_t)((1u << c->n) - 1u);
+    static cco_path st[CCO_STACK_DEPTH];
+    unsigned size = 1, cur = 0;
+    int status = 0;
+    memset(st, 0, sizeof st);
+    for (size_t t = 1; t <= T; ++t) {
+        if (soft) memcpy(fbuf + (t - 1) * NS, rx + (t - 1) * NS, NS * sizeof(float));
+        else hbuf[t - 1] = syms[t - 1] & mask;
+        const uint16_t W = soft ? (uint16_t)(t * NS) : (uint16_t)(uint8_t)t;
+        for (;;) {
+            /* get_most_probable_path: strict >, first index wins */
+            cur = size;
+            float fmax = -INFINITY;
+            int32_t imax = (int32_t)0x80000000;
+            for (unsigned i = 0; i < size; ++i)
+                if (soft ? (st[i].fmetric > fmax) : (st[i].imetric > imax)) {
+                    fmax = st[i].fmetric; imax = st[i].imetric; cur = i;
+                }
+            if (cur == size) return -1;   /* no finite metric: the reference reads past its stack */
+            if (st[cur].next == W) break;
+            const unsigned idx = st[cur].next;
+            if (idx + NS > T * NS) return -1;   /* past the input buffer */
+            uint64_t ns[2];
+            float ftm[2] = {0, 0};
+            int32_t itm[2] = {0, 0};
+            for (int in = 0; in < 2; ++in) {
+                int e = stack_symbol(c, st[cur].state, in, &ns[in]);
+                if (soft) {
+                    ftm[in] = (float)(1.0 + (double)(weight * fbuf[idx + (unsigned)e]));
+                } else {
+                    int32_t d = __builtin_popcount((unsigned)(e ^ hbuf[idx]));
+                    itm[in] = d * bm[1] + (c->n - d) * bm[0];
+                }
+            }
+            /* duplicate_path */
+            unsigned lhs;
+            if (size == CCO_STACK_DEPTH) {
+                lhs = size;
+                float fmin = INFINITY;
+                int32_t imin = 0x7FFFFFFF;
+                for (unsigned i = 0; i < size; ++i)
+                    if (soft ? (st[i].fmetric < fmin) : (st[i].imetric < imin)) {
+                        fmin = st[i].fmetric; imin = st[i].imetric; lhs = i;
+                    }
+                if (lhs == size) return -1;
+            } else {
+                lhs = size++;
+            }
+            if (lhs != cur) st[lhs] = st[cur];
+            for (int in = 0; in < 2; ++in) {
+                cco_path* p = &st[in ? lhs : cur];
+                unsigned w = (uint8_t)(p->next / NS);
+                p->next = (uint16_t)(p->next + NS);
+                if (!soft) p->next &= 0xFF;
+                p->state = ns[in];
+                if (soft) p->fmetric += ftm[in];
+                else p->imetric += itm[in];
+                if (w / 8 < sizeof p->path) p->path[w / 8] |= (uint8_t)(in << (7 - w % 8));
+            }
+        }
+    }
+    memcpy(out, st[cur].path, OB);
+    if (pm) *pm = st[cur].imetric;
+    return status;
+}
+
+int cco_stack_soft(const cco_code* c, float metric_weight, const float* rx, size_t nblocks,
+                   uint8_t* out) {
+    size_t T = cco_steps(c), NS = (size_t)1 << c->n, OB = cco_out_bytes(c);
+    float* buf = (float*)calloc(T * NS, sizeof(float));
+    int rc = 0;
+    for (size_t b = 0; b < nblocks; ++b)
+        if (stack_block(c, 1, metric_weight, NULL, rx + b * T * NS, NULL, buf, NULL, out + b * OB, NULL))
+            rc = -1;
+    free(buf);
+    return rc;
+}
+
+int cco_stack_hard(const cco_code* c, const int32_t* bit_metrics, const uint8_t* syms, size_t nblocks,
+                   uint8_t* out, int32_t* path_metric) {
+    size_t T = cco_steps(c), OB = cco_out_bytes(c);
+    uint8_t* buf = (uint8_t*)calloc(T, 1);
+    int rc = 0;
+    for (size_t b = 0; b < nblocks; ++b)
+        if (stack_block(c, 0, 0.0f, bit_metrics, NULL, syms + b * T, NULL, buf, out + b * OB,
+                        path_metric ? path_metric + b : NULL))
+            rc = -1;
+    free(buf);
+    return rc;
+}
+
 /* AWGN-channel/main.c:129-141: compare the first blen bits, MSB-first. */
 uint64_t cco_count_errors(const cco_code* c, const uint8_t* info, const uint8_t* out, size_t nblocks) {
     size_t IB = cco_info_bytes(c), OB = cco_out_bytes(c);

@@ -71,6 +71,17 @@ void     cco_viterbi_soft(const cco_code* c, const float* rx, size_t nblocks, ui
 void     cco_viterbi_hard(const cco_code* c, const uint8_t* syms, size_t nblocks, uint8_t* out,
                           int32_t* path_metric /* [nb] */);
 
+/* Stack (sequential) decoders, AWGN-channel/stack-decoder.c and binary-symmetric-channel/
+ * stack-decoder.c: 64-entry path stack, extend the most probable path until it spans the block.
+ * Soft branch metric (float)(1.0 + weight * d[sym]); hard: d * bit_metrics[1] + (n - d) *
+ * bit_metrics[0] with d the Hamming distance. Blocks run through one decoder in order (a path that
+ * overtakes the received frontier reads the previous block's symbols, as in the reference). Returns
+ * -1 if some block made the reference read past its buffers. Requires T <= 255 and K <= 64. */
+int      cco_stack_soft(const cco_code* c, float metric_weight, const float* rx, size_t nblocks,
+                        uint8_t* out /* [nb][OB] */);
+int      cco_stack_hard(const cco_code* c, const int32_t* bit_metrics /* [2] */, const uint8_t* syms,
+                        size_t nblocks, uint8_t* out, int32_t* path_metric /* [nb] */);
+
 /* Consumer: bit errors over the first blen bits of each block (AWGN-channel/main.c:118-144). */
 uint64_t cco_count_errors(const cco_code* c, const uint8_t* info, const uint8_t* out, size_t nblocks);
 

@@ -7,9 +7,12 @@
  * data crossing the decoder boundary: info bytes, the decoder's input stream, the decoder's output
  * buffer (all ceil(T/8) bytes, tail bits included), the BSC path metric and the bit-error count.
  *
- * usage: ref_harness_{awgn,bsc} OUTPREFIX SEED NBLOCKS CHANNELPARAM CODESPEC
+ * usage: ref_harness_{awgn,bsc}[_stack] OUTPREFIX SEED NBLOCKS CHANNELPARAM CODESPEC [METRICS]
  *   CHANNELPARAM: AWGN noise scaling factor (float) | BSC crossover probability in ppm (int)
  *   CODESPEC:     cb:<codebook index>  |  n:K:blen:poly0hex:poly1hex[:poly2hex]
+ *   METRICS:      stack decoder metrics overriding the codebook's (code.h:14-16):
+ *                 AWGN metric_weight (float) | BSC bit_metrics "m0,m1"
+ * The same harness is linked against viterbi-decoder.c or stack-decoder.c (oracle/Makefile).
  * writes OUTPREFIX.info .rx .out [.pm] .meta
  */
 #include <stdint.h>
@@ -100,6 +103,7 @@ static int on_decoded(uint8_t* data, uint8_t len, int32_t path_metric, void* ud)
 #endif
 
 static uint64_t custom_polys[8];
+static int32_t custom_bit_metrics[2];
 
 static int parse_code(const char* spec, struct code_param* p) {
     if (strncmp(spec, "cb:", 3) == 0) {
@@ -133,8 +137,8 @@ static FILE* open_out(const char* prefix, const char* ext) {
 }
 
 int main(int argc, char** argv) {
-    if (argc != 6) {
-        fprintf(stderr, "usage: %s OUTPREFIX SEED NBLOCKS CHANNELPARAM CODESPEC\n", argv[0]);
+    if (argc != 6 && argc != 7) {
+        fprintf(stderr, "usage: %s OUTPREFIX SEED NBLOCKS CHANNELPARAM CODESPEC [METRICS]\n", argv[0]);
         return 2;
     }
     const char* prefix = argv[1];
@@ -145,8 +149,13 @@ int main(int argc, char** argv) {
     if (parse_code(argv[5], &h.param) != 0) { fprintf(stderr, "bad code spec\n"); return 2; }
 #ifdef HARNESS_AWGN
     h.scaling = (float)atof(argv[4]);
+    if (argc == 7) h.param.metric_weight = (float)atof(argv[6]);
 #else
     h.p_ppm = (int32_t)atol(argv[4]);
+    if (argc == 7) {
+        if (sscanf(argv[6], "%d,%d", &custom_bit_metrics[0], &custom_bit_metrics[1]) != 2) return 2;
+        h.param.bit_metrics = custom_bit_metrics;
+    }
 #endif
     h.param.userdata = &h;
     h.encoder = encoder_create();
@@ -185,6 +194,9 @@ int main(int argc, char** argv) {
             (unsigned long long)h.errors, h.param.symlen_out, h.param.constr_len, h.param.block_len);
     for (int k = 0; k < h.param.symlen_out; ++k)
         fprintf(meta, "poly%d %016llx\n", k, (unsigned long long)h.param.polynomials[k]);
+    fprintf(meta, "metric_weight %.9g\n", (double)h.param.metric_weight);
+    fprintf(meta, "bit_metric0 %d\nbit_metric1 %d\n", h.param.bit_metrics ? h.param.bit_metrics[0] : 0,
+            h.param.bit_metrics ? h.param.bit_metrics[1] : 0);
     fclose(meta);
     return h.block == (size_t)nblocks ? 0 : 1;
 }

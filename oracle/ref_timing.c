@@ -1,8 +1,9 @@
 /*
  * ref_timing.c -- TEST/BENCH INFRASTRUCTURE ONLY. CPU baseline for bench.py.
  *
- * Built by oracle/Makefile into oracle/_ref/libccref_{awgn,bsc}.so together with the UNMODIFIED
- * reference decoder (AWGN-channel/viterbi-decoder.c or binary-symmetric-channel/viterbi-decoder.c).
+ * Built by oracle/Makefile into oracle/_ref/libccref_{awgn,bsc}[_stack].so together with an UNMODIFIED
+ * reference decoder (AWGN-channel/viterbi-decoder.c or binary-symmetric-channel/viterbi-decoder.c, or
+ * the stack-decoder.c of either channel).
  * It feeds pre-generated decoder input to the reference decoder one trellis step per decoder_input()
  * call, as the reference drivers do (AWGN-channel/main.c:108-116, binary-symmetric-channel/main.c:70),
  * on NTHREADS threads, one decoder handle per thread (the decoder keeps no globals), and returns the
@@ -28,6 +29,15 @@ typedef struct {
     int rc;
 } job_t;
 
+/* Stack-decoder builds (libccref_*_stack.so): code_param's stack metrics (code.h:14-16). */
+static float g_metric_weight = -15.0f;
+static int32_t g_bit_metrics[2] = {1, -15};
+void ccref_set_stack_metrics(float metric_weight, int32_t bm0, int32_t bm1) {
+    g_metric_weight = metric_weight;
+    g_bit_metrics[0] = bm0;
+    g_bit_metrics[1] = bm1;
+}
+
 #ifdef TIMING_AWGN
 static int on_decoded(uint8_t* data, uint8_t len, void* ud) {
     (void)len;
@@ -52,6 +62,8 @@ static void* run_job(void* arg) {
     struct decoder* d = decoder_create();
     j->param.userdata = j;
     j->param.polynomials = j->polys;
+    j->param.metric_weight = g_metric_weight;
+    j->param.bit_metrics = g_bit_metrics;
     if (!d || decoder_init(d, &j->param) != 0) { j->rc = -1; return NULL; }
     decoder_register_callback(d, on_decoded);
     const uint8_t* base = (const uint8_t*)j->in + j->first * j->steps * j->in_step_bytes;

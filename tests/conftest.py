@@ -15,8 +15,9 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
 
 
-def golden_manifest():
-    with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
+def golden_manifest(kind="viterbi"):
+    name = "manifest.json" if kind == "viterbi" else "manifest_stack.json"
+    with open(os.path.join(REPO, "tests", "golden", name)) as f:
         return json.load(f)
 
 

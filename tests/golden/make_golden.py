@@ -6,7 +6,7 @@ reference sources in place into oracle/_ref/ref_harness_{awgn,bsc} (driver logic
 and this script runs them with fixed seeds and packs what crossed the decoder boundary into one .npz
 per case (plain arrays, loaded with allow_pickle=False). The GPU box never runs this script.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--stack-only]
 """
 import json
 import os
@@ -59,11 +59,33 @@ CASES = [
     ("awgn_n1k3_4dB", "awgn", "1:3:40:E000000000000000", 216, 50, SCALING[4]),
 ]
 
+# K=15 r=1/2 (46321,51271)_8 for BASELINE config 5 (the codebook has no K=15 code); the metric weight
+# is the codebook's long-code (WSPR, K=32) value, codebook.c:71-73.
+K15 = "2:15:{blen}:" + "%016X:%016X" % (0o46321 << 49, 0o51271 << 49)
 
-def run_case(name, channel, spec, seed, nblocks, param, tmp):
-    exe = os.path.join(REF_DIR, f"ref_harness_{channel}")
+# Stack-decoder cases (manifest_stack.json): (name, channel, code spec, seed, nblocks, channel
+# parameter, metrics override or None = the codebook's)
+STACK_CASES = [
+    ("stack_awgn_cb0_4dB", "awgn", "cb:0", 301, 200, SCALING[4], None),
+    ("stack_awgn_cb0_8dB", "awgn", "cb:0", 302, 200, SCALING[8], None),
+    ("stack_awgn_cb3_2dB", "awgn", "cb:3", 303, 100, SCALING[2], None),
+    ("stack_awgn_cb4_4dB", "awgn", "cb:4", 304, 60, SCALING[4], None),
+    ("stack_awgn_cb5_4dB", "awgn", "cb:5", 305, 100, SCALING[4], None),
+    ("stack_awgn_k15_4dB", "awgn", K15.format(blen=40), 306, 100, SCALING[4], "-7.0"),
+    ("stack_awgn_k15_2dB", "awgn", K15.format(blen=40), 307, 60, SCALING[2], "-7.0"),
+    ("stack_awgn_k7_blen200_4dB", "awgn", K7.format(blen=200), 308, 20, SCALING[4], "-10.0"),
+    ("stack_bsc_cb0_p25000", "bsc", "cb:0", 401, 200, "25000", None),
+    ("stack_bsc_cb2_p50000", "bsc", "cb:2", 402, 100, "50000", None),
+    ("stack_bsc_cb4_p20000", "bsc", "cb:4", 403, 60, "20000", None),
+    ("stack_bsc_k15_p30000", "bsc", K15.format(blen=40), 404, 100, "30000", "1,-11"),
+]
+
+
+def run_case(name, channel, spec, seed, nblocks, param, tmp, decoder="viterbi", metrics=None):
+    exe = os.path.join(REF_DIR, f"ref_harness_{channel}" + ("_stack" if decoder == "stack" else ""))
     prefix = os.path.join(tmp, name)
-    subprocess.run([exe, prefix, str(seed), str(nblocks), param, spec], check=True, timeout=120)
+    cmd = [exe, prefix, str(seed), str(nblocks), param, spec] + ([metrics] if metrics else [])
+    subprocess.run(cmd, check=True, timeout=600)
     meta = {}
     with open(prefix + ".meta") as f:
         for line in f:
@@ -86,9 +108,15 @@ def run_case(name, channel, spec, seed, nblocks, param, tmp):
         arrays["rx"] = np.fromfile(prefix + ".rx", dtype=np.uint8).reshape(nblocks, T)
         arrays["p_ppm"] = np.int32(int(param))
         arrays["path_metric"] = np.fromfile(prefix + ".pm", dtype=np.int32).reshape(nblocks)
+    if decoder == "stack":
+        arrays["metric_weight"] = np.float32(float(meta["metric_weight"]))
+        arrays["bit_metrics"] = np.array([int(meta["bit_metric0"]), int(meta["bit_metric1"])], np.int32)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
-    return {"name": name, "channel": channel, "spec": spec, "seed": seed, "nblocks": nblocks,
-            "param": param, "errors": int(meta["errors"])}
+    entry = {"name": name, "channel": channel, "spec": spec, "seed": seed, "nblocks": nblocks,
+             "param": param, "errors": int(meta["errors"])}
+    if decoder == "stack":
+        entry.update(decoder="stack", metrics=metrics)
+    return entry
 
 
 def main():
@@ -97,11 +125,19 @@ def main():
     subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     manifest = []
     with tempfile.TemporaryDirectory() as tmp:
-        for case in CASES:
+        for case in ([] if "--stack-only" in sys.argv else CASES):
             manifest.append(run_case(*case, tmp))
             print(manifest[-1])
-    with open(os.path.join(HERE, "manifest.json"), "w") as f:
-        json.dump(manifest, f, indent=1)
+    if manifest:
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1)
+    stack = []
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, channel, spec, seed, nb, param, metrics in STACK_CASES:
+            stack.append(run_case(name, channel, spec, seed, nb, param, tmp, "stack", metrics))
+            print(stack[-1])
+    with open(os.path.join(HERE, "manifest_stack.json"), "w") as f:
+        json.dump(stack, f, indent=1)
 
 
 if __name__ == "__main__":

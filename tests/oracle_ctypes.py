@@ -52,6 +52,10 @@ def lib():
         L.cco_viterbi_soft.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.cco_viterbi_hard.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_void_p]
+        L.cco_stack_soft.argtypes = [P(CcoCode), ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p]
+        L.cco_stack_hard.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p, ctypes.c_void_p]
         L.cco_count_errors.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         L.cco_count_errors.restype = ctypes.c_uint64
         _lib = L
@@ -111,6 +115,28 @@ def viterbi_hard(c, syms):
     out = np.zeros((syms.shape[0], OB), np.uint8)
     pm = np.zeros(syms.shape[0], np.int32)
     lib().cco_viterbi_hard(ctypes.byref(c), _ptr(syms), syms.shape[0], _ptr(out), _ptr(pm))
+    return out, pm
+
+
+def stack_soft(c, metric_weight, rx):
+    """Stack decoder restatement (AWGN-channel/stack-decoder.c)."""
+    rx = np.ascontiguousarray(rx, dtype=np.float32)
+    _, _, OB = dims(c)
+    out = np.zeros((rx.shape[0], OB), np.uint8)
+    if lib().cco_stack_soft(ctypes.byref(c), float(metric_weight), _ptr(rx), rx.shape[0], _ptr(out)):
+        raise RuntimeError("the reference would read past its buffers on some block")
+    return out
+
+
+def stack_hard(c, bit_metrics, syms):
+    """Stack decoder restatement (binary-symmetric-channel/stack-decoder.c); (out, path metric)."""
+    syms = np.ascontiguousarray(syms, dtype=np.uint8)
+    bm = np.ascontiguousarray(bit_metrics, dtype=np.int32)
+    _, _, OB = dims(c)
+    out = np.zeros((syms.shape[0], OB), np.uint8)
+    pm = np.zeros(syms.shape[0], np.int32)
+    if lib().cco_stack_hard(ctypes.byref(c), _ptr(bm), _ptr(syms), syms.shape[0], _ptr(out), _ptr(pm)):
+        raise RuntimeError("the reference would read past its buffers on some block")
     return out, pm
 
 

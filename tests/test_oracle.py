@@ -34,6 +34,29 @@ def test_oracle_matches_reference_fixture(case):
     assert O.count_errors(c, g["info"], out) == int(g["errors"]) == case["errors"]
 
 
+STACK_CASES = golden_manifest("stack")
+
+
+@pytest.mark.parametrize("case", STACK_CASES, ids=[c["name"] for c in STACK_CASES])
+def test_stack_oracle_matches_reference_fixture(case):
+    """Stack-decoder restatement vs the unmodified reference stack-decoder.c on the same inputs."""
+    g = O.load_golden(case["name"])
+    c = O.golden_code(g)
+    nb = g["info"].shape[0]
+    if case["channel"] == "awgn":
+        info, rx = O.awgn_blocks(c, int(g["seed"]), float(g["scaling"]), nb)
+        assert np.array_equal(rx.view(np.uint32), g["rx"].view(np.uint32))
+        out = O.stack_soft(c, float(g["metric_weight"]), g["rx"])
+    else:
+        info, syms = O.bsc_blocks(c, int(g["seed"]), int(g["p_ppm"]), nb)
+        assert np.array_equal(syms, g["rx"])
+        out, pm = O.stack_hard(c, g["bit_metrics"], g["rx"])
+        assert np.array_equal(pm, g["path_metric"])
+    assert np.array_equal(info, g["info"])
+    assert np.array_equal(out, g["out"])
+    assert O.count_errors(c, g["info"], out) == int(g["errors"]) == case["errors"]
+
+
 def test_rand_restatement_matches_glibc():
     libc = ctypes.CDLL(ctypes.util.find_library("c"))
     for seed in (1, 2, 12345, 0xC0DE, 2**31 - 1):
