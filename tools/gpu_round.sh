@@ -14,6 +14,9 @@ rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 3 > $OUT/bench.log 2>&1 && timeout -k 10 300 python bench.py --steps $STEPS --warmup 3 --layout step --no-cpu-baseline > $OUT/bench_step.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 $OUT/bench.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python bench.py --code k9 --frames 16 --steps $STEPS --warmup 3 --no-cpu-baseline > $OUT/bench_k9.log 2>&1 && \
+timeout -k 10 300 python bench.py --decoder stack --frames 4 --steps 5 --warmup 1 > $OUT/bench_stack.log 2>&1
+rc=$?; echo "extra benches rc=$rc"; tail -1 $OUT/bench_k9.log | cut -c1-200; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
     python bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && { tail -20 $OUT/prof.log; exit $rc; }
