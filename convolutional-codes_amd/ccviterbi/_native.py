@@ -72,7 +72,8 @@ def core():
     L.ccv_plan_reserve.restype = _i
     L.ccv_decode_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
     L.ccv_decode_device.restype = _i
-    L.ccv_simulate_device.argtypes = [_vp, _u64, _u64, _sz, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.ccv_simulate_device.argtypes = [_vp, _u64, _u64, _sz, ctypes.c_double, _u, _vp, _vp, _vp, _vp,
+                                      _vp, _vp]
     L.ccv_simulate_device.restype = _i
     L.ccv_stack_plan_create.argtypes = [_P(_vp), _i, _i, _i, _i, _P(_u64), _i, ctypes.c_float, _vp]
     L.ccv_stack_plan_create.restype = _i

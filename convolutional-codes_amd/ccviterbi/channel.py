@@ -49,9 +49,14 @@ def demap(n: int, iq: np.ndarray) -> np.ndarray:
     return rx
 
 
+DEMAP_HARD = 0x100   # CCV_DEMAP_HARD: common/hard-demapper.c instead of common/demapper.c
+
+
 def awgn_blocks(code: Code, nblocks: int, scaling: float, seed: int, rng: int = RNG_PHILOX,
-                first_block: int = 0, threads: int = None, info=None, rx=None):
+                first_block: int = 0, threads: int = None, info=None, rx=None, hard_demap=False):
     """(info uint8 [nb, IB], rx float32 [nb, T, 2^n]); `info`/`rx` may be preallocated views."""
+    if hard_demap:
+        rng |= DEMAP_HARD
     if info is None:
         info = np.empty((nblocks, code.info_bytes), np.uint8)
     if rx is None:

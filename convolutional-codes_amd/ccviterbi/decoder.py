@@ -89,11 +89,13 @@ class Plan:
             raise DecoderError(f"ccv_decode_device: {_native.last_error()}")
 
     def simulate_device(self, seed, first_block, nblocks, channel_param, d_errors=None, d_info=None,
-                        d_out=None, d_path_metric=None, d_channel=None, stream=None):
+                        d_out=None, d_path_metric=None, d_channel=None, stream=None, hard_demap=False):
         """On-device channel + decode (ccv_simulate_device): blocks first_block.. of the Philox stream
-        `seed`; channel_param = AWGN noise scaling (soft plan) or BSC p_ppm (hard plan)."""
+        `seed`; channel_param = AWGN noise scaling (soft plan) or BSC p_ppm (hard plan); hard_demap
+        selects the reference's hard demapper (common/hard-demapper.c)."""
         rc = self._lib.ccv_simulate_device(self._h, int(seed), int(first_block), int(nblocks),
-                                           float(channel_param), _ptr(d_info), _ptr(d_out),
+                                           float(channel_param), 1 if hard_demap else 0,
+                                           _ptr(d_info), _ptr(d_out),
                                            _ptr(d_path_metric), _ptr(d_errors), _ptr(d_channel),
                                            _stream_handle(stream))
         if rc != 0:

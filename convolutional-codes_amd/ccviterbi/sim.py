@@ -92,7 +92,8 @@ class DeviceChannelDecoder:
     """Frames generated AND decoded on the current GPU (ccv_simulate_device): the same Philox frames
     as the host producers, no host generation and no input traffic."""
 
-    def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None):
+    def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None,
+                 hard_demap=False):
         import torch
 
         from .decoder import Plan
@@ -101,6 +102,7 @@ class DeviceChannelDecoder:
         self.plan = Plan(code, channel)
         self.plan.reserve(frame_blocks)
         self.channel, self.frame_blocks, self.seed = channel, frame_blocks, seed
+        self.hard_demap = hard_demap
         self.d_err = torch.zeros(1, dtype=torch.int64, device=self.device)
 
     def __call__(self, point: float, first_blocks: Sequence[int]) -> int:
@@ -110,7 +112,7 @@ class DeviceChannelDecoder:
         stream = self.torch.cuda.current_stream(self.device)
         for first in first_blocks:
             self.plan.simulate_device(self.seed, first, self.frame_blocks, param, d_errors=self.d_err,
-                                      stream=stream)
+                                      stream=stream, hard_demap=self.hard_demap)
         return int(self.d_err.item())
 
 
@@ -119,7 +121,7 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
               seed: int = 0xC0DE, rank: int = 0, world: int = 1,
               decode: Optional[Callable[[np.ndarray, np.ndarray], int]] = None,
               threads: Optional[int] = None, reduce: bool = True,
-              device_channel: bool = False) -> List[BerPoint]:
+              device_channel: bool = False, hard_demap: bool = False) -> List[BerPoint]:
     """BER at each point; `decode(info, data) -> errors` defaults to the GPU decoder. With
     device_channel the frames are generated on the GPU as well (DeviceChannelDecoder)."""
     if bits_per_point is None:
@@ -127,7 +129,8 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
             bits_per_point = lambda p: reference_awgn_bits(p, code.blen)   # noqa: E731
         else:
             bits_per_point = lambda p: reference_bsc_bits(int(p), code.blen)  # noqa: E731
-    dev = DeviceChannelDecoder(code, channel, frame_blocks, seed) if device_channel else None
+    dev = DeviceChannelDecoder(code, channel, frame_blocks, seed, hard_demap=hard_demap) \
+        if device_channel else None
     if decode is None and dev is None:
         decode = GpuFrameDecoder(code, channel, frame_blocks)
     counters = np.zeros((len(points), 2), np.int64)
@@ -142,7 +145,7 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
             first = (pi << 40) + f * frame_blocks
             if channel == SOFT:
                 info, data = ch.awgn_blocks(code, frame_blocks, ch.noise_scaling(p), seed,
-                                            first_block=first, threads=threads)
+                                            first_block=first, threads=threads, hard_demap=hard_demap)
             else:
                 info, data = ch.bsc_blocks(code, frame_blocks, int(p), seed, first_block=first,
                                            threads=threads)

@@ -3,7 +3,8 @@
 // demapper -- or the BSC bit flips -- generated per lane, step by step, in the order the decoder
 // consumes them, so no channel data touches HBM. The draw sequence is the product's host Philox
 // producer's (csrc/sim.cpp PhiloxSource / Gauss / awgn_block / bsc_block), which follows the
-// reference drivers' rand() call order:
+// reference drivers' rand() call order (optionally through the hard demapper,
+// common/hard-demapper.c:62-102):
 //   AWGN-channel/main.c:217-223 (info bytes, rand() % 256), :93-106 (per symbol: map, add
 //   scaling * gengauss() per I/Q in double, demap); common/gaussian.c:18-38 (Box-Muller, cosine
 //   half first, u1 == 0 redrawn); common/demapper.c:61-70 (squared distance / ndist in fp32);
@@ -30,6 +31,7 @@ struct ChanArgs {
   uint64_t first_block;      // block b of the batch is stream block first_block + b
   float scaling;             // AWGN: noise scaling (AWGN-channel/main.c:157-161)
   int32_t p_ppm;             // BSC: flip probability in ppm
+  int hard_demap;            // AWGN: common/hard-demapper.c instead of common/demapper.c
   uint8_t* info_out;         // [nb][IB] transmitted info bytes (required)
   void* ch_out;              // optional export: soft float [nb][T][2^n] / hard uint8 [nb][T]
 };
@@ -130,12 +132,13 @@ struct ChannelSource {
   int T, blen;
   float scaling;
   int32_t p_ppm;
+  bool hard_demap;
   void* out;       // export row of this block, or null
 
   // Draw the info bytes (first in the stream), write them to info_out, prime the encoder.
   __device__ __forceinline__ void init(const ChanArgs& a, int block, bool owner) {
     T = a.r.T; blen = a.r.blen;
-    scaling = a.scaling; p_ppm = a.p_ppm;
+    scaling = a.scaling; p_ppm = a.p_ppm; hard_demap = a.hard_demap != 0;
     rng.init(a.seed, a.first_block + (uint64_t)block);
     const int IB = (blen + 7) >> 3;
 #pragma unroll
@@ -203,6 +206,21 @@ struct ChannelSource {
       sincos(Tt, &sn, &cs);
       x = (float)((double)x + (double)scaling * (R * cs));
       y = (float)((double)y + (double)scaling * (R * sn));
+      if (hard_demap) {   // common/hard-demapper.c:66-80: snap to the first nearest point
+        float min_val = __builtin_inff();
+        float sx = pts[0], sy = pts[1];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          const float dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
+          const float d = (dx * dx) + (dy * dy);
+          const bool lt = d < min_val;
+          min_val = lt ? d : min_val;
+          sx = lt ? pts[2 * k] : sx;
+          sy = lt ? pts[2 * k + 1] : sy;
+        }
+        x = sx;
+        y = sy;
+      }
       constexpr float ndx = pts[0] - pts[2], ndy = pts[1] - pts[3];
       constexpr float nd = (ndx * ndx) + (ndy * ndy);
 #pragma unroll

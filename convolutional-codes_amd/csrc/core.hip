@@ -424,8 +424,9 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
 }
 
 int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t nblocks,
-                        double channel_param, uint8_t* d_info, uint8_t* d_out, int32_t* d_path_metric,
-                        unsigned long long* d_errors, void* d_channel, void* stream_v) {
+                        double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,
+                        int32_t* d_path_metric, unsigned long long* d_errors, void* d_channel,
+                        void* stream_v) {
   if (!p) return fail("null plan");
   if (p->stack) return fail("the on-device channel is implemented for the Viterbi kernels");
   if (!register_path(*p))
@@ -462,6 +463,8 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   a.first_block = first_block;
   a.scaling = (float)channel_param;
   a.p_ppm = hard ? (int32_t)channel_param : 0;
+  a.hard_demap = (channel_flags & CCV_CHANNEL_HARD_DEMAP) != 0;
+  if (hard && a.hard_demap) return fail("the hard demapper belongs to the AWGN channel");
   a.info_out = d_info;
   a.ch_out = d_channel;
   const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);

@@ -71,6 +71,23 @@ inline void demap(int n, const float* pts, float ndist, float x, float y, float*
   }
 }
 
+// common/hard-demapper.c:62-88: snap to the nearest point (strict <, first minimum), then the
+// normalised squared distances from that point.
+inline void demap_hard(int n, const float* pts, float ndist, float x, float y, float* out) {
+  float min_val = INFINITY;
+  int min_idx = 0;
+  for (int k = 0; k < (1 << n); ++k) {
+    float dx = x - pts[2 * k];
+    float dy = y - pts[2 * k + 1];
+    float d = (dx * dx) + (dy * dy);
+    if (d < min_val) {
+      min_val = d;
+      min_idx = k;
+    }
+  }
+  demap(n, pts, ndist, pts[2 * min_idx], pts[2 * min_idx + 1], out);
+}
+
 float ndist_of(const float* pts) {
   float dx = pts[0] - pts[2];
   float dy = pts[1] - pts[3];
@@ -154,7 +171,7 @@ struct Gauss {
 // One AWGN block in driver order (AWGN-channel/main.c:217-223 then :93-106 per symbol).
 template <class Src>
 void awgn_block(const Code& c, Src& src, Gauss<Src>& g, float scaling, const float* pts, float nd,
-                uint8_t* info, float* rx) {
+                bool hard, uint8_t* info, float* rx) {
   uint8_t syms[512];
   for (int j = 0; j < c.IB; ++j) info[j] = (uint8_t)(src.next() % 256);
   c.encode(info, syms);
@@ -163,7 +180,8 @@ void awgn_block(const Code& c, Src& src, Gauss<Src>& g, float scaling, const flo
     float x = pts[2 * syms[t]], y = pts[2 * syms[t] + 1];
     x = (float)((double)x + (double)scaling * g.next());
     y = (float)((double)y + (double)scaling * g.next());
-    demap(c.n, pts, nd, x, y, rx + (size_t)t * NS);
+    if (hard) demap_hard(c.n, pts, nd, x, y, rx + (size_t)t * NS);
+    else demap(c.n, pts, nd, x, y, rx + (size_t)t * NS);
   }
 }
 
@@ -226,12 +244,14 @@ int ccv_sim_awgn(int n, int K, int blen, const uint64_t* polys, int gen_mode, in
   if (!c.init(n, K, blen, polys, gen_mode) || !pts || !info || !rx) return -1;
   const float nd = ndist_of(pts);
   const size_t rx_per_block = (size_t)c.T << n;
+  const bool hard = (rng & CCV_DEMAP_HARD) != 0;
+  rng &= ~CCV_DEMAP_HARD;
   if (rng == CCV_RNG_GLIBC) {
     if (first_block != 0) return -1;
     GlibcSource src(seed);
     Gauss<GlibcSource> g(src);
     for (size_t b = 0; b < nblocks; ++b)
-      awgn_block(c, src, g, scaling, pts, nd, info + b * c.IB, rx + b * rx_per_block);
+      awgn_block(c, src, g, scaling, pts, nd, hard, info + b * c.IB, rx + b * rx_per_block);
     return 0;
   }
   if (rng != CCV_RNG_PHILOX) return -1;
@@ -239,7 +259,7 @@ int ccv_sim_awgn(int n, int K, int blen, const uint64_t* polys, int gen_mode, in
     for (size_t b = lo; b < hi; ++b) {
       PhiloxSource src(seed, first_block + b);
       Gauss<PhiloxSource> g(src);
-      awgn_block(c, src, g, scaling, pts, nd, info + b * c.IB, rx + b * rx_per_block);
+      awgn_block(c, src, g, scaling, pts, nd, hard, info + b * c.IB, rx + b * rx_per_block);
     }
   });
   return 0;

@@ -93,9 +93,11 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
  * d_errors and d_channel (export of the decoder input: float [nb][T][2^n] or uint8 [nb][T]) may be
  * NULL; info and output then go to plan-owned scratch. Info bits and BSC symbols are bit-identical
  * to ccv_sim_*; AWGN samples use the device's double log/sin/cos. Asynchronous on `stream`. */
+#define CCV_CHANNEL_HARD_DEMAP 1u   /* AWGN: common/hard-demapper.c instead of common/demapper.c */
 int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
-                        double channel_param, uint8_t* d_info, uint8_t* d_out, int32_t* d_path_metric,
-                        unsigned long long* d_errors, void* d_channel, void* stream);
+                        double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,
+                        int32_t* d_path_metric, unsigned long long* d_errors, void* d_channel,
+                        void* stream);
 
 /* Stack (sequential) decoder plan (AWGN-channel/stack-decoder.c, binary-symmetric-channel/
  * stack-decoder.c): 64-entry path stack, K <= 64. metric_weight = code_param.metric_weight (soft),

@@ -26,6 +26,9 @@ extern "C" {
 
 #define CCV_RNG_GLIBC 0
 #define CCV_RNG_PHILOX 1
+/* OR into ccv_sim_awgn's rng argument: demap with common/hard-demapper.c (snap to the nearest point,
+ * then distances from it) instead of common/demapper.c. */
+#define CCV_DEMAP_HARD 0x100
 
 /* Encoder only: syms = uint8 [nblocks][T] from info = uint8 [nblocks][ceil(blen/8)]. */
 int ccv_sim_encode(int n, int K, int blen, const uint64_t* polys, int gen_mode, const uint8_t* info,

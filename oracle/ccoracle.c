@@ -141,10 +141,27 @@ void cco_demap(int n, float x, float y, float* out) {
     }
 }
 
+/* common/hard-demapper.c:62-88: snap to the nearest constellation point (strict <, first minimum),
+ * then the normalised squared distances from that point. */
+void cco_demap_hard(int n, float x, float y, float* out) {
+    float pts[16];
+    cco_constellation(n, pts);
+    float min_val = INFINITY;
+    int min_idx = 0;
+    for (int k = 0; k < (1 << n); ++k) {
+        float dx = x - pts[2 * k];
+        float dy = y - pts[2 * k + 1];
+        float d = (dx * dx) + (dy * dy);
+        if (d < min_val) { min_val = d; min_idx = k; }
+    }
+    cco_demap(n, pts[2 * min_idx], pts[2 * min_idx + 1], out);
+}
+
 /* AWGN-channel/main.c:212-229 (info bytes by rand()%256), :93-106 (noise added per I/Q sample in
- * double, stored back to float), common/mapper.c:54-71, common/demapper.c:61-85. */
-void cco_awgn_blocks(const cco_code* c, uint32_t seed, float scaling, size_t nblocks, uint8_t* info,
-                     float* rx) {
+ * double, stored back to float), common/mapper.c:54-71, common/demapper.c:61-85 or, hard != 0,
+ * common/hard-demapper.c:62-102. */
+void cco_awgn_blocks_demap(const cco_code* c, uint32_t seed, float scaling, size_t nblocks, int hard,
+                           uint8_t* info, float* rx) {
     cco_rng g;
     cco_srand(&g, seed);
     size_t T = cco_steps(c), IB = cco_info_bytes(c), NS = (size_t)1 << c->n;
@@ -159,9 +176,15 @@ void cco_awgn_blocks(const cco_code* c, uint32_t seed, float scaling, size_t nbl
             float x = pts[2 * syms[t]], y = pts[2 * syms[t] + 1];
             x = (float)((double)x + (double)scaling * cco_gengauss(&g));
             y = (float)((double)y + (double)scaling * cco_gengauss(&g));
-            cco_demap(c->n, x, y, rx + (b * T + t) * NS);
+            if (hard) cco_demap_hard(c->n, x, y, rx + (b * T + t) * NS);
+            else cco_demap(c->n, x, y, rx + (b * T + t) * NS);
         }
     }
+}
+
+void cco_awgn_blocks(const cco_code* c, uint32_t seed, float scaling, size_t nblocks, uint8_t* info,
+                     float* rx) {
+    cco_awgn_blocks_demap(c, seed, scaling, nblocks, 0, info, rx);
 }
 
 /* binary-symmetric-channel/main.c:57-72 (per-bit flips with rand()%1000000 < p) and :159-172. */

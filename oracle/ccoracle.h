@@ -58,11 +58,14 @@ size_t   cco_out_bytes(const cco_code* c);      /* ceil(T/8) */
 void     cco_encode_block(const cco_code* c, const uint8_t* info, uint8_t* syms /* [T] */);
 void     cco_constellation(int n, float* pts /* [2 * 2^n] */);
 void     cco_demap(int n, float x, float y, float* out /* [2^n] */);
+void     cco_demap_hard(int n, float x, float y, float* out /* [2^n] */);
 
 /* Driver-order channels (AWGN-channel/main.c:80-116,212-229; binary-symmetric-channel/main.c:57-72,
  * 159-172) starting from srand(seed). */
 void     cco_awgn_blocks(const cco_code* c, uint32_t seed, float scaling, size_t nblocks,
                          uint8_t* info /* [nb][IB] */, float* rx /* [nb][T][2^n] */);
+void     cco_awgn_blocks_demap(const cco_code* c, uint32_t seed, float scaling, size_t nblocks, int hard,
+                               uint8_t* info, float* rx);   /* hard: common/hard-demapper.c */
 void     cco_bsc_blocks(const cco_code* c, uint32_t seed, int32_t p_ppm, size_t nblocks,
                         uint8_t* info /* [nb][IB] */, uint8_t* syms /* [nb][T] */);
 

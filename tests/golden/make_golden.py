@@ -6,7 +6,7 @@ reference sources in place into oracle/_ref/ref_harness_{awgn,bsc} (driver logic
 and this script runs them with fixed seeds and packs what crossed the decoder boundary into one .npz
 per case (plain arrays, loaded with allow_pickle=False). The GPU box never runs this script.
 
-    python tests/golden/make_golden.py [--stack-only]
+    python tests/golden/make_golden.py [--stack-only | --hd-only]
 """
 import json
 import os
@@ -59,6 +59,14 @@ CASES = [
     ("awgn_n1k3_4dB", "awgn", "1:3:40:E000000000000000", 216, 50, SCALING[4]),
 ]
 
+# AWGN through the reference's hard demapper (common/hard-demapper.c linked instead of demapper.c):
+# (name, channel, code spec, seed, nblocks, channel parameter); manifest entries carry demapper "hard"
+HD_CASES = [
+    ("awgn_hd_cb0_4dB", "awgn", "cb:0", 501, 200, SCALING[4]),
+    ("awgn_hd_cb5_6dB", "awgn", "cb:5", 502, 100, SCALING[6]),
+    ("awgn_hd_k7_4dB", "awgn", K7.format(blen=40), 503, 100, SCALING[4]),
+]
+
 # K=15 r=1/2 (46321,51271)_8 for BASELINE config 5 (the codebook has no K=15 code); the metric weight
 # is the codebook's long-code (WSPR, K=32) value, codebook.c:71-73.
 K15 = "2:15:{blen}:" + "%016X:%016X" % (0o46321 << 49, 0o51271 << 49)
@@ -81,8 +89,10 @@ STACK_CASES = [
 ]
 
 
-def run_case(name, channel, spec, seed, nblocks, param, tmp, decoder="viterbi", metrics=None):
-    exe = os.path.join(REF_DIR, f"ref_harness_{channel}" + ("_stack" if decoder == "stack" else ""))
+def run_case(name, channel, spec, seed, nblocks, param, tmp, decoder="viterbi", metrics=None,
+             demapper="soft"):
+    suffix = ("_stack" if decoder == "stack" else "") + ("_hd" if demapper == "hard" else "")
+    exe = os.path.join(REF_DIR, f"ref_harness_{channel}{suffix}")
     prefix = os.path.join(tmp, name)
     cmd = [exe, prefix, str(seed), str(nblocks), param, spec] + ([metrics] if metrics else [])
     subprocess.run(cmd, check=True, timeout=600)
@@ -116,6 +126,8 @@ def run_case(name, channel, spec, seed, nblocks, param, tmp, decoder="viterbi", 
              "param": param, "errors": int(meta["errors"])}
     if decoder == "stack":
         entry.update(decoder="stack", metrics=metrics)
+    if demapper == "hard":
+        entry.update(demapper="hard")
     return entry
 
 
@@ -124,13 +136,23 @@ def main():
         sys.exit("make_golden.py needs /root/reference (build container only)")
     subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     manifest = []
+    only_new = "--stack-only" in sys.argv or "--hd-only" in sys.argv
     with tempfile.TemporaryDirectory() as tmp:
-        for case in ([] if "--stack-only" in sys.argv else CASES):
+        for case in ([] if only_new else CASES):
             manifest.append(run_case(*case, tmp))
             print(manifest[-1])
+        if "--stack-only" not in sys.argv:
+            if only_new:   # append to the existing manifest without rewriting the other fixtures
+                with open(os.path.join(HERE, "manifest.json")) as f:
+                    manifest = [m for m in json.load(f) if m.get("demapper") != "hard"]
+            for case in HD_CASES:
+                manifest.append(run_case(*case, tmp, demapper="hard"))
+                print(manifest[-1])
     if manifest:
         with open(os.path.join(HERE, "manifest.json"), "w") as f:
             json.dump(manifest, f, indent=1)
+    if "--hd-only" in sys.argv:
+        return
     stack = []
     with tempfile.TemporaryDirectory() as tmp:
         for name, channel, spec, seed, nb, param, metrics in STACK_CASES:

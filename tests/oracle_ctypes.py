@@ -47,6 +47,8 @@ def lib():
         L.cco_demap.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
         L.cco_awgn_blocks.argtypes = [P(CcoCode), ctypes.c_uint32, ctypes.c_float, ctypes.c_size_t,
                                       ctypes.c_void_p, ctypes.c_void_p]
+        L.cco_awgn_blocks_demap.argtypes = [P(CcoCode), ctypes.c_uint32, ctypes.c_float, ctypes.c_size_t,
+                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.cco_bsc_blocks.argtypes = [P(CcoCode), ctypes.c_uint32, ctypes.c_int32, ctypes.c_size_t,
                                      ctypes.c_void_p, ctypes.c_void_p]
         L.cco_viterbi_soft.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
@@ -85,11 +87,12 @@ def trellis(c):
     return out
 
 
-def awgn_blocks(c, seed, scaling, nblocks):
+def awgn_blocks(c, seed, scaling, nblocks, hard_demap=False):
     T, IB, _ = dims(c)
     info = np.zeros((nblocks, IB), np.uint8)
     rx = np.zeros((nblocks, T, 1 << c.n), np.float32)
-    lib().cco_awgn_blocks(ctypes.byref(c), seed, scaling, nblocks, _ptr(info), _ptr(rx))
+    lib().cco_awgn_blocks_demap(ctypes.byref(c), seed, scaling, nblocks, 1 if hard_demap else 0,
+                                _ptr(info), _ptr(rx))
     return info, rx
 
 

@@ -415,7 +415,7 @@ def test_reference_driver_with_mi355x_decoder(case, tmp_path):
 
 # --------------------------------------------------------------- on-device channel (ccv_simulate_device)
 
-def _simulate(torch, plan, c, seed, first, nb, param):
+def _simulate(torch, plan, c, seed, first, nb, param, hard_demap=False):
     hard = plan.channel == HARD
     d_info = torch.empty((nb, c.info_bytes), dtype=torch.uint8, device="cuda")
     d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
@@ -424,7 +424,7 @@ def _simulate(torch, plan, c, seed, first, nb, param):
     shape = (nb, c.steps) if hard else (nb, c.steps, 1 << c.n)
     d_ch = torch.empty(shape, dtype=torch.uint8 if hard else torch.float32, device="cuda")
     plan.simulate_device(seed, first, nb, param, d_errors=d_err, d_info=d_info, d_out=d_out,
-                         d_path_metric=d_pm if hard else None, d_channel=d_ch)
+                         d_path_metric=d_pm if hard else None, d_channel=d_ch, hard_demap=hard_demap)
     torch.cuda.synchronize()
     return (d_info.cpu().numpy(), d_ch.cpu().numpy(), d_out.cpu().numpy(), d_pm.cpu().numpy(),
             int(d_err.item()))
@@ -462,6 +462,21 @@ def test_device_channel_awgn(torch_cuda, name, c):
     exact = np.mean(rx == h_rx)
     assert exact >= 0.999, exact
     assert np.allclose(rx, h_rx, rtol=1e-5, atol=1e-6)
+    assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
+    assert err == ch.count_bit_errors(c, info, out)
+
+
+@pytest.mark.parametrize("name,c", CHANNEL_CODES[:5], ids=[x[0] for x in CHANNEL_CODES[:5]])
+def test_device_channel_awgn_hard_demapper(torch_cuda, name, c):
+    """The reference's hard demapper (common/hard-demapper.c) on the device: decoder input equal to
+    the host producer's (both snap to the nearest point; a sample may land on the other side of a
+    decision boundary only where device and glibc libm round differently), decode bit-exact."""
+    nb = 300
+    scaling = ch.noise_scaling(3.0)
+    info, rx, out, _, err = _simulate(torch_cuda, Plan(c, SOFT), c, 9, 4321, nb, scaling, hard_demap=True)
+    h_info, h_rx = ch.awgn_blocks(c, nb, scaling, 9, first_block=4321, hard_demap=True)
+    assert np.array_equal(info, h_info)
+    assert np.mean(np.all(rx == h_rx, axis=2)) >= 0.999
     assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
     assert err == ch.count_bit_errors(c, info, out)
 

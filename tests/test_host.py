@@ -30,7 +30,8 @@ def test_producers_reproduce_reference_inputs(case):
     c = _code_of(g)
     nb = g["info"].shape[0]
     if case["channel"] == "awgn":
-        info, rx = ch.awgn_blocks(c, nb, float(g["scaling"]), int(g["seed"]), rng=ch.RNG_GLIBC)
+        info, rx = ch.awgn_blocks(c, nb, float(g["scaling"]), int(g["seed"]), rng=ch.RNG_GLIBC,
+                                  hard_demap=case.get("demapper") == "hard")
         assert np.array_equal(rx.view(np.uint32), g["rx"].view(np.uint32))
     else:
         info, syms = ch.bsc_blocks(c, nb, int(g["p_ppm"]), int(g["seed"]), rng=ch.RNG_GLIBC)

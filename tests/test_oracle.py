@@ -19,7 +19,8 @@ def test_oracle_matches_reference_fixture(case):
     nb = g["info"].shape[0]
     # producers: the reference driver's rand() stream from srand(seed), bit for bit
     if case["channel"] == "awgn":
-        info, rx = O.awgn_blocks(c, int(g["seed"]), float(g["scaling"]), nb)
+        info, rx = O.awgn_blocks(c, int(g["seed"]), float(g["scaling"]), nb,
+                                 hard_demap=case.get("demapper") == "hard")
         assert np.array_equal(rx.view(np.uint32), g["rx"].view(np.uint32))
         out = O.viterbi_soft(c, g["rx"])
     else:
