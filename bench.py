@@ -44,17 +44,22 @@ def cpu_threads():
     return max(1, min(16, n))
 
 
-def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, stack=False):
+def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi"):
     """Reference decoder (oracle/_ref, compiled from the reference's own sources) on host cores,
     over a bounded sample of the SAME frames the GPU decodes; its output is checked against the GPU's.
     Falls back to the oracle restatement ("port", one thread) where oracle/_ref was not built."""
-    ref_so = os.path.join(REPO, "oracle", "_ref", "libccref_awgn_stack.so" if stack else "libccref_awgn.so")
+    stack = decoder == "stack"
+    suffix = "" if decoder == "viterbi" else "_" + decoder
+    ref_so = os.path.join(REPO, "oracle", "_ref", f"libccref_awgn{suffix}.so")
     polys = (ctypes.c_uint64 * code.n)(*code.polys)
     if os.path.exists(ref_so):
         lib = ctypes.CDLL(ref_so)
-        if stack:
+        if decoder != "viterbi":
             lib.ccref_set_stack_metrics.argtypes = [ctypes.c_float, ctypes.c_int32, ctypes.c_int32]
-            lib.ccref_set_stack_metrics(code.metric_weight, *code.bit_metrics)
+            if stack:
+                lib.ccref_set_stack_metrics(code.metric_weight, *code.bit_metrics)
+            else:
+                lib.ccref_set_stack_metrics(code.fano_metric_weight, *code.fano_bit_metrics)
         lib.ccref_decode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -78,7 +83,12 @@ def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, stack=False):
 
         def run(nb, nthr):
             t0 = time.perf_counter()
-            out = O.stack_soft(oc, code.metric_weight, rx[:nb]) if stack else O.viterbi_soft(oc, rx[:nb])
+            if decoder == "stack":
+                out = O.stack_soft(oc, code.metric_weight, rx[:nb])
+            elif decoder == "fano":
+                out = O.fano_soft(oc, code.fano_metric_weight, rx[:nb])
+            else:
+                out = O.viterbi_soft(oc, rx[:nb])
             return time.perf_counter() - t0, out
         kind = "port"
     t_cal, _ = run(200, 1)                      # calibrate: seconds per block on one core
@@ -125,8 +135,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--code", default=None,
                     help="k7 (default), k9, k15 (stack default), code0..code5; suffix :true = true parity")
-    ap.add_argument("--decoder", choices=("viterbi", "stack"), default="viterbi",
-                    help="viterbi (BASELINE configs 1-4) or the stack decoder (config 5, K=15)")
+    ap.add_argument("--decoder", choices=("viterbi", "stack", "fano"), default="viterbi",
+                    help="viterbi (BASELINE configs 1-4), the stack decoder (config 5, K=15) or Fano")
     ap.add_argument("--frames", type=int, default=64,
                     help="1 M-bit frames per GPU per step (64 = 1.6 M blocks = 25,000 one-wave tiles, "
                          "~6 waves per SIMD so the last partial round is a small fraction)")
@@ -144,7 +154,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from ccviterbi import SOFT, Plan, StackPlan, channel as ch, named_code
+    from ccviterbi import SOFT, FanoPlan, Plan, StackPlan, channel as ch, named_code
     from ccviterbi.decoder import FLAG_STEP_MAJOR
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -157,10 +167,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     stack = args.decoder == "stack"
+    sequential = args.decoder != "viterbi"
     if args.code is None:
-        args.code = "k15" if stack else "k7"
-    if stack and args.layout != "block":
-        raise SystemExit("the stack decoder reads block-major input")
+        args.code = "k15" if sequential else "k7"
+    if sequential and args.layout != "block":
+        raise SystemExit("the sequential decoders read block-major input")
     code = named_code(args.code)
     nb = args.frames * FRAME_BLOCKS
     # this rank's frames: blocks [rank*nb, (rank+1)*nb) of the Philox stream
@@ -171,7 +182,12 @@ def main():
     d_info = torch.from_numpy(info).to("cuda")
     d_out = torch.empty((nb, code.out_bytes), dtype=torch.uint8, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
-    plan = StackPlan(code, SOFT) if stack else Plan(code, SOFT, FLAG_STEP_MAJOR if args.layout == "step" else 0)
+    if args.decoder == "stack":
+        plan = StackPlan(code, SOFT)
+    elif args.decoder == "fano":
+        plan = FanoPlan(code, SOFT)
+    else:
+        plan = Plan(code, SOFT, FLAG_STEP_MAJOR if args.layout == "step" else 0)
     plan.reserve(nb)
     stream = torch.cuda.current_stream()
 
@@ -218,7 +234,7 @@ def main():
     # informational: the same frames generated AND decoded on the GPU (ccv_simulate_device, the
     # on-device channel of SURVEY.md 8(f) #1) -- no host producer, no input in HBM
     fused = None
-    if rank == 0 and not args.no_fused_channel and not stack:
+    if rank == 0 and not args.no_fused_channel and not sequential:
         d_ferr = torch.zeros(1, dtype=torch.int64, device="cuda")
         scaling = ch.noise_scaling(args.ebn0)
         plan.simulate_device(args.seed, 0, nb, scaling, d_errors=d_ferr, stream=stream)   # warm-up
@@ -246,14 +262,14 @@ def main():
     errors = int(errs.item())
 
     if rank == 0:
-        bpb = algorithmic_bytes_per_bit(code, decisions=not stack)
+        bpb = algorithmic_bytes_per_bit(code, decisions=not sequential)
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         workload_key = f"{args.code}:frames{args.frames}:{args.layout}"
         traffic = load_pmc_traffic(workload_key)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, _ = cpu_baseline(code, rx, d_out.cpu().numpy(), args.cpu_seconds, stack=stack)
+            cpu, _ = cpu_baseline(code, rx, d_out.cpu().numpy(), args.cpu_seconds, decoder=args.decoder)
         line = {
             "metric": METRIC,
             "value": round(bits_per_step * args.steps / wall / 1e6, 2),
@@ -270,7 +286,8 @@ def main():
                     "resident in HBM before timing",
             "config": {
                 "workload": f"awgn-simulation {code.name or args.code} r=1/{code.n} K={code.K} soft "
-                            f"{'stack decoder' if stack else 'Viterbi'}, blen {code.blen}, "
+                            f"{ {'stack': 'stack decoder', 'fano': 'Fano decoder'}.get(args.decoder, 'Viterbi')}, "
+                            f"blen {code.blen}, "
                             f"{args.frames} x 1M-bit frames per GPU per step",
                 "code": args.code,
                 "generator": "ref-x86" if code.gen_mode == 0 else "true-parity",

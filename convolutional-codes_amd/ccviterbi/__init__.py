@@ -6,11 +6,11 @@ libccv_sim.so holds the CPU-side producers. This package is the Python host mirr
 """
 from .code import (CODEBOOK, GEN_REF_X86, GEN_TRUE_PARITY, HARD, K7, K8, K9, K15, SOFT, STANDARD, Code,
                    CodeParam, get_code, named_code)
-from .decoder import DecoderError, HardDecoder, Plan, SoftDecoder, StackPlan, device_count
+from .decoder import DecoderError, FanoPlan, HardDecoder, Plan, SoftDecoder, StackPlan, device_count
 from ._native import NativeLibraryError
 
 __all__ = [
     "CODEBOOK", "GEN_REF_X86", "GEN_TRUE_PARITY", "HARD", "K7", "K8", "K9", "K15", "SOFT", "STANDARD",
     "Code", "CodeParam", "get_code", "named_code", "DecoderError", "HardDecoder", "Plan",
-    "SoftDecoder", "StackPlan", "device_count", "NativeLibraryError",
+    "SoftDecoder", "StackPlan", "FanoPlan", "device_count", "NativeLibraryError",
 ]

@@ -79,6 +79,10 @@ def core():
     L.ccv_stack_plan_create.restype = _i
     L.ccv_stack_decode_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.ccv_stack_decode_device.restype = _i
+    L.ccv_fano_plan_create.argtypes = [_P(_vp), _i, _i, _i, _i, _P(_u64), _i, ctypes.c_float, _vp]
+    L.ccv_fano_plan_create.restype = _i
+    L.ccv_fano_decode_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.ccv_fano_decode_device.restype = _i
     L.ccv_decode_host.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.ccv_decode_host.restype = _i
     L.ccv_device_count.argtypes = []

@@ -97,7 +97,8 @@ K8 = Code(2, 8, 40, (_octal_to_msb(0o371, 8), _octal_to_msb(0o247, 8)), name="k8
 # BASELINE config 5: K=15 r=1/2 (46321,51271)_8 for the stack decoder; the codebook has no K=15 code,
 # so its stack metrics borrow the codebook's long-code (WSPR K=32) weight (codebook.c:71-73).
 K15 = Code(2, 15, 40, (_octal_to_msb(0o46321, 15), _octal_to_msb(0o51271, 15)), metric_weight=-7.0,
-           bit_metrics=(1, -11), name="k15_46321_51271")
+           bit_metrics=(1, -11), fano_metric_weight=-11.0, fano_bit_metrics=(1, -11),
+           name="k15_46321_51271")
 STANDARD = {"k7": K7, "k8": K8, "k9": K9, "k15": K15}
 
 

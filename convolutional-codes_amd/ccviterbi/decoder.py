@@ -15,7 +15,7 @@ import numpy as np
 from . import _native
 from .code import GEN_REF_X86, HARD, SOFT, Code
 
-KERNEL_REGISTER, KERNEL_GENERIC, KERNEL_MULTILANE, KERNEL_STACK = 1, 2, 3, 4
+KERNEL_REGISTER, KERNEL_GENERIC, KERNEL_MULTILANE, KERNEL_STACK, KERNEL_FANO = 1, 2, 3, 4, 5
 FLAG_GENERIC = 1
 FLAG_STEP_MAJOR = 2
 
@@ -68,7 +68,8 @@ class Plan:
     @property
     def kernel(self):
         return {KERNEL_REGISTER: "register", KERNEL_GENERIC: "generic",
-                KERNEL_MULTILANE: "multilane", KERNEL_STACK: "stack"}[self.desc.kernel]
+                KERNEL_MULTILANE: "multilane", KERNEL_STACK: "stack",
+                KERNEL_FANO: "fano"}[self.desc.kernel]
 
     def trellis(self) -> np.ndarray:
         out = np.zeros((self.desc.states, 2), np.uint8)
@@ -157,6 +158,35 @@ class StackPlan(Plan):
             self.close()
         except Exception:
             pass
+
+
+class FanoPlan(Plan):
+    """Fano decoder plan (ccv_fano_plan_create): AWGN-channel/fano-decoder.c or
+    binary-symmetric-channel/fano-decoder.c with the code's fano_metric_weight / fano_bit_metrics."""
+
+    def __init__(self, code: Code, channel: int = SOFT):
+        self.code = code
+        self.channel = channel
+        self._lib = _native.core()
+        self._polys = code.poly_array()
+        self._bm = (ctypes.c_int32 * 2)(*code.fano_bit_metrics)
+        h = ctypes.c_void_p()
+        if self._lib.ccv_fano_plan_create(ctypes.byref(h), channel, code.n, code.K, code.blen,
+                                          self._polys, code.gen_mode, float(code.fano_metric_weight),
+                                          self._bm) != 0:
+            raise DecoderError(f"ccv_fano_plan_create: {_native.last_error()}")
+        self._h = h
+        self.desc = _native.CcvPlanDesc()
+        self._lib.ccv_plan_describe(self._h, ctypes.byref(self.desc))
+
+    def decode_fano_device(self, d_in, nblocks, d_out, d_path_metric=None, d_info=None, d_errors=None,
+                           d_iterations=None, stream=None):
+        """ccv_fano_decode_device; d_iterations[nb] = search iterations (10000 * T = timeout)."""
+        rc = self._lib.ccv_fano_decode_device(self._h, _ptr(d_in), int(nblocks), _ptr(d_out),
+                                              _ptr(d_path_metric), _ptr(d_info), _ptr(d_errors),
+                                              _ptr(d_iterations), _stream_handle(stream))
+        if rc != 0:
+            raise DecoderError(f"ccv_fano_decode_device: {_native.last_error()}")
 
 
 _SOFT_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint8, ctypes.c_void_p)

@@ -1,9 +1,10 @@
 // api_shim.cpp -- reference-compatible decoder_* API over libccv_core.
 //
-// Compiled four times: -DCCV_SHIM_AWGN -> libccv_awgn.so (include/decoder_awgn.h) and
+// Compiled six times: -DCCV_SHIM_AWGN -> libccv_awgn.so (include/decoder_awgn.h) and
 // -DCCV_SHIM_BSC -> libccv_bsc.so (include/decoder_bsc.h) replace the Viterbi decoders; with
 // -DCCV_SHIM_STACK added -> libccv_stack_{awgn,bsc}.so replace the stack decoders
-// (AWGN-channel/stack-decoder.c, binary-symmetric-channel/stack-decoder.c; same decoder.h). Life
+// (AWGN-channel/stack-decoder.c, binary-symmetric-channel/stack-decoder.c; same decoder.h); with
+// -DCCV_SHIM_FANO -> libccv_fano_{awgn,bsc}.so replace the Fano decoders (fano-decoder.c). Life
 // cycle and semantics follow AWGN-channel/viterbi-decoder.c:143-236 and
 // binary-symmetric-channel/viterbi-decoder.c:152-243 (stack-decoder.c:45-197 alike): streaming
 // input, a block completes after block_len + K - 1 steps, the output callback fires synchronously
@@ -133,7 +134,14 @@ CCV_EXPORT int decoder_init(struct decoder* obj, struct code_param* param) {
   obj->parameter = *param;   // by value; the polynomial array stays borrowed (reference :169)
   ccv_plan_destroy(obj->plan);
   obj->plan = nullptr;
-#if defined(CCV_SHIM_STACK)
+#if defined(CCV_SHIM_FANO)
+  if (CCV_CHANNEL == CCV_HARD && param->fano_bit_metrics == nullptr)
+    return shim_fail("null fano_bit_metrics");
+  if (ccv_fano_plan_create(&obj->plan, CCV_CHANNEL, param->symlen_out, param->constr_len,
+                           param->block_len, param->polynomials, obj->gen_mode,
+                           param->fano_metric_weight, param->fano_bit_metrics) != 0)
+    return shim_fail(ccv_last_error());
+#elif defined(CCV_SHIM_STACK)
   // stack-decoder.c:74-103 reallocates its input buffer: no streaming context survives init
   obj->prev_valid = false;
   if (CCV_CHANNEL == CCV_HARD && param->bit_metrics == nullptr) return shim_fail("null bit_metrics");

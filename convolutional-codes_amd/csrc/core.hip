@@ -9,6 +9,7 @@
 
 #include "acs_generic.hpp"
 #include "channel_dev.hpp"
+#include "fano_dev.hpp"
 #include "stack_dev.hpp"
 #include "ccv.h"
 #include "reg_codes.hpp"
@@ -16,6 +17,7 @@
 
 namespace ccv {
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s);   // stack.hip
+hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s);     // stack.hip
 }
 
 namespace {
@@ -70,6 +72,8 @@ struct ccv_plan {
   int reg_index = -1;                // kRegCodes index, or -1
   int multi_index = -1;              // kMultiCodes index (K = 8, 9), or -1
   bool stack = false;                // stack (sequential) decoder plan
+  bool fano = false;                 // Fano decoder plan
+  DeviceBuffer counter;              // Fano: block work counter
   float metric_weight = 0.0f;        // stack, soft: code_param.metric_weight
   int32_t bit_metrics[2] = {0, 0};   // stack, hard: code_param.bit_metrics
   bool step_major = false;           // soft input layout [T][nblocks][2^n] (CCV_FLAG_STEP_MAJOR)
@@ -254,6 +258,7 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->host_pm.release();
   p->sim_info.release();
   p->sim_out.release();
+  p->counter.release();
   if (p->d_exp) (void)hipFree(p->d_exp);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -286,6 +291,11 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
   if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
   hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
   const bool hard = p->d.channel == CCV_HARD;
+  if (p->fano) {
+    if (d_decisions) return fail("a Fano decoder has no survivor decisions");
+    return ccv_fano_decode_device(p, d_in, nblocks, d_out, d_path_metric, d_info, d_errors, nullptr,
+                                  stream_v);
+  }
   if (p->stack) {
     if (d_decisions) return fail("a stack decoder has no survivor decisions");
     return ccv_stack_decode_device(p, d_in, nblocks, nullptr, d_out, d_path_metric, d_info, d_errors,
@@ -339,9 +349,26 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
   return 0;
 }
 
+static int sequential_plan_create(ccv_plan** out, bool fano, int channel, int n, int K, int blen,
+                                  const uint64_t* polys, int gen_mode, float metric_weight,
+                                  const int32_t* bit_metrics);
+
 int ccv_stack_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const uint64_t* polys,
                           int gen_mode, float metric_weight, const int32_t* bit_metrics) {
-  if (!out) return fail("ccv_stack_plan_create: null output pointer");
+  return sequential_plan_create(out, false, channel, n, K, blen, polys, gen_mode, metric_weight,
+                                bit_metrics);
+}
+
+int ccv_fano_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const uint64_t* polys,
+                         int gen_mode, float fano_metric_weight, const int32_t* fano_bit_metrics) {
+  return sequential_plan_create(out, true, channel, n, K, blen, polys, gen_mode, fano_metric_weight,
+                                fano_bit_metrics);
+}
+
+static int sequential_plan_create(ccv_plan** out, bool fano, int channel, int n, int K, int blen,
+                                  const uint64_t* polys, int gen_mode, float metric_weight,
+                                  const int32_t* bit_metrics) {
+  if (!out) return fail("plan create: null output pointer");
   *out = nullptr;
   if (channel != CCV_SOFT && channel != CCV_HARD) return fail("bad channel %d", channel);
   if (n < 1 || n > ccv::kMaxN) return fail("n=%d unsupported (1..%d)", n, ccv::kMaxN);
@@ -351,15 +378,16 @@ int ccv_stack_plan_create(ccv_plan** out, int channel, int n, int K, int blen, c
   if (gen_mode != CCV_GEN_REF_X86 && gen_mode != CCV_GEN_TRUE_PARITY)
     return fail("bad generator mode %d", gen_mode);
   const int T = blen + K - 1;
-  if (channel == CCV_HARD && T > 255)
-    return fail("T=%d > 255: the BSC stack decoder's uint8_t indices wrap", T);
+  if (T > 255)   // uint8_t blocklen_w_tail / input indices (stack-decoder.c:15, fano-decoder.c:36)
+    return fail("T=%d > 255: the reference decoder's uint8_t step indices wrap", T);
   if (channel == CCV_HARD && !bit_metrics) return fail("null bit metrics");
-  if (channel == CCV_SOFT && ((size_t)T << n) > 65535)
+  if (!fano && channel == CCV_SOFT && ((size_t)T << n) > 65535)
     return fail("T * 2^n = %zu floats: the AWGN stack decoder's uint16_t index wraps", (size_t)T << n);
-  if (channel == CCV_SOFT && 2 * ((size_t)T << n) * sizeof(float) > 64 * 1024)
+  if (!fano && channel == CCV_SOFT && 2 * ((size_t)T << n) * sizeof(float) > 64 * 1024)
     return fail("T * 2^n too large for the staged input (64 KiB of LDS)");
   ccv_plan* p = new ccv_plan();
-  p->stack = true;
+  p->stack = !fano;
+  p->fano = fano;
   p->metric_weight = metric_weight;
   if (bit_metrics) {
     p->bit_metrics[0] = bit_metrics[0];
@@ -375,8 +403,8 @@ int ccv_stack_plan_create(ccv_plan** out, int channel, int n, int K, int blen, c
   p->d.info_bytes = (blen + 7) / 8;
   p->d.out_bytes = (T + 7) / 8;
   p->d.in_step_bytes = channel == CCV_SOFT ? (int)sizeof(float) << n : 1;
-  p->d.kernel = CCV_KERNEL_STACK;
-  p->d.lanes = ccv::kStackDepth;
+  p->d.kernel = fano ? CCV_KERNEL_FANO : CCV_KERNEL_STACK;
+  p->d.lanes = fano ? 1 : ccv::kStackDepth;
   memcpy(p->polys, polys, sizeof(uint64_t) * (size_t)n);
   hipError_t e = hipGetDevice(&p->d.device);
   if (e != hipSuccess) {
@@ -390,6 +418,39 @@ int ccv_stack_plan_create(ccv_plan** out, int channel, int n, int K, int blen, c
     return fail("hipStreamCreate failed");
   }
   *out = p;
+  return 0;
+}
+
+int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_out,
+                           int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
+                           uint32_t* d_iterations, void* stream_v) {
+  if (!p) return fail("null plan");
+  if (!p->fano) return fail("not a Fano-decoder plan (ccv_fano_plan_create)");
+  if (nblocks == 0) return 0;
+  if (!d_in || !d_out) return fail("null device buffer");
+  if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+  if (p->counter.grow(sizeof(unsigned int), stream)) return -1;
+  HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, sizeof(unsigned int), stream));
+  ccv::FanoArgs a{};
+  a.in = d_in;
+  a.n = p->d.n;
+  a.K = p->d.K;
+  a.T = p->d.steps;
+  a.blen = p->d.blen;
+  a.gen = p->d.gen_mode;
+  memcpy(a.poly, p->polys, sizeof a.poly);
+  a.weight = p->metric_weight;
+  a.bm0 = p->bit_metrics[0];
+  a.bm1 = p->bit_metrics[1];
+  a.nblocks = (int)nblocks;
+  a.next_block = static_cast<unsigned int*>(p->counter.ptr);
+  a.out = d_out;
+  a.path_metric = p->d.channel == CCV_HARD ? d_path_metric : nullptr;
+  a.info = d_info;
+  a.err = d_info ? d_errors : nullptr;
+  a.iterations = d_iterations;
+  HIP_TRY(ccv::launch_fano(a, p->d.channel == CCV_HARD, stream));
   return 0;
 }
 
@@ -428,7 +489,8 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
                         int32_t* d_path_metric, unsigned long long* d_errors, void* d_channel,
                         void* stream_v) {
   if (!p) return fail("null plan");
-  if (p->stack) return fail("the on-device channel is implemented for the Viterbi kernels");
+  if (p->stack || p->fano)
+    return fail("the on-device channel is implemented for the Viterbi kernels");
   if (!register_path(*p))
     return fail("the on-device channel needs a register-trellis code (K <= 9 with a specialised kernel)");
   if (p->d.channel == CCV_SOFT && p->d.n > 3)

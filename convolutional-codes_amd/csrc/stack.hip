@@ -1,5 +1,7 @@
-// stack.hip -- launches of the wave-per-block stack decoder (stack_dev.hpp). Built with
-// -ffp-contract=off: the branch metric's float product and double sum must not fuse.
+// stack.hip -- launches of the sequential decoders: the wave-per-block stack decoder (stack_dev.hpp)
+// and the lane-per-block Fano decoder (fano_dev.hpp). Built with -ffp-contract=off: the branch
+// metrics' float product and double sum must not fuse.
+#include "fano_dev.hpp"
 #include "stack_dev.hpp"
 
 namespace ccv {
@@ -34,6 +36,29 @@ hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
   if (pw <= 4) return launch_pw<false, 4>(a, lds, s);
   if (pw <= 8) return launch_pw<false, 8>(a, lds, s);
   return launch_pw<false, 10>(a, lds, s);
+}
+
+template <bool HARD, int NP, bool W32>
+static hipError_t launch_fano_v(const FanoArgs& a, int grid, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((fano_decode<HARD, NP, W32>), dim3(grid), dim3(kFanoThreads), lds, s, a);
+  return hipGetLastError();
+}
+
+template <bool HARD>
+static hipError_t launch_fano_h(const FanoArgs& a, int grid, size_t lds, hipStream_t s) {
+  if (a.K <= 32) {
+    if (a.n == 2) return launch_fano_v<HARD, 2, true>(a, grid, lds, s);
+    if (a.n == 3) return launch_fano_v<HARD, 3, true>(a, grid, lds, s);
+  }
+  return launch_fano_v<HARD, 0, false>(a, grid, lds, s);
+}
+
+// Persistent lanes: enough waves to fill the chip (LDS permitting), each lane pulls blocks.
+hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
+  const size_t lds = (size_t)a.T * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1);
+  const int waves_needed = (a.nblocks + kFanoThreads - 1) / kFanoThreads;
+  const int grid = waves_needed < 4096 ? waves_needed : 4096;
+  return hard ? launch_fano_h<true>(a, grid, lds, s) : launch_fano_h<false>(a, grid, lds, s);
 }
 
 }  // namespace ccv

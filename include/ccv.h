@@ -43,6 +43,7 @@ extern "C" {
 #define CCV_KERNEL_GENERIC 2  /* table-driven LDS kernel                                        */
 #define CCV_KERNEL_MULTILANE 3 /* K = 8, 9: register-trellis kernel, 2^(K-7) lanes per block      */
 #define CCV_KERNEL_STACK 4    /* stack (sequential) decoder, one wave per block                  */
+#define CCV_KERNEL_FANO 5     /* Fano decoder, one persistent lane per block                     */
 
 typedef struct ccv_plan ccv_plan;
 
@@ -113,6 +114,20 @@ int ccv_stack_plan_create(ccv_plan** plan, int channel, int n, int K, int blen, 
 int ccv_stack_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, const void* d_prev,
                             uint8_t* d_out, int32_t* d_path_metric, const uint8_t* d_info,
                             unsigned long long* d_errors, int32_t* d_status, void* stream);
+
+/* Fano decoder plan (AWGN-channel/fano-decoder.c, binary-symmetric-channel/fano-decoder.c): threshold
+ * search with DELTA 17 and a timeout of 10000 iterations per block bit, K <= 64, T <= 255.
+ * fano_metric_weight = code_param.fano_metric_weight (soft), fano_bit_metrics = code_param.
+ * fano_bit_metrics[2] (hard; code.h:15-17). ccv_decode_device / ccv_decode_host accept the plan
+ * (hard: d_path_metric = the reference callback's path metric). */
+int ccv_fano_plan_create(ccv_plan** plan, int channel, int n, int K, int blen, const uint64_t* polys,
+                         int gen_mode, float fano_metric_weight, const int32_t* fano_bit_metrics);
+
+/* Fano decode with the per-block search length exported: d_iterations[nb] (optional) = iterations
+ * used; 10000 * T means the block hit the reference's timeout. */
+int ccv_fano_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t* d_out,
+                           int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
+                           uint32_t* d_iterations, void* stream);
 
 /* Host-buffer form of ccv_stack_decode_device (prev, path_metric, status may be NULL). */
 int ccv_stack_decode_host(ccv_plan* plan, const void* in, size_t nblocks, const void* prev,

@@ -428,6 +428,137 @@ int cco_stack_hard(const cco_code* c, const int32_t* bit_metrics, const uint8_t*
     return rc;
 }
 
+/* ---------------------------------------------------------------- Fano decoders */
+
+#define CCO_FANO_TIMEOUT 10000   /* fano-decoder.c:14, cycles per decoded bit */
+
+typedef struct {
+    uint64_t state;
+    float fmetric;
+    int32_t imetric;
+    uint8_t sel;                 /* selected_path */
+    float ftm[2];
+    int32_t itm[2];
+    uint64_t succ[2];
+    uint8_t decoded;             /* decoded_input */
+} cco_fano_node;
+
+/* get_transition_metric (AWGN-channel/fano-decoder.c:282-313 / BSC :284-320) and the sort that
+ * follows it (:169-181 / :224-236): best transition first, decoded_input = 1 if input 1 is best. */
+static void fano_node_metrics(const cco_code* c, int soft, float fw, const int32_t* fbm, const float* r,
+                              uint8_t rsym, cco_fano_node* nd) {
+    for (int in = 0; in < 2; ++in) {
+        int e = stack_symbol(c, nd->state, in, &nd->succ[in]);
+        if (soft) {
+            nd->ftm[in] = (float)(1.0 + (double)(fw * r[e]));
+        } else {
+            int32_t d = __builtin_popcount((unsigned)(e ^ rsym));
+            nd->itm[in] = d * fbm[1] + (c->n - d) * fbm[0];
+        }
+    }
+    if (soft ? (nd->ftm[0] < nd->ftm[1]) : (nd->itm[0] < nd->itm[1])) {
+        uint64_t st = nd->succ[0]; nd->succ[0] = nd->succ[1]; nd->succ[1] = st;
+        float ft = nd->ftm[0]; nd->ftm[0] = nd->ftm[1]; nd->ftm[1] = ft;
+        int32_t it = nd->itm[0]; nd->itm[0] = nd->itm[1]; nd->itm[1] = it;
+        nd->decoded = 1;
+    }
+}
+
+/* One block of the Fano search (fano-decoder.c:108-124 reset, :140-273 receive_symbol, :315-325
+ * output), written for a fully received block: the streaming loop returns whenever the search first
+ * reaches the newest node and resumes there when its symbol arrives, where it computes exactly what
+ * the forward move would (the node is fresh), so the operation sequence and the per-block timeout
+ * count are the same. BSC path metric: the metric of the newest received node when the search ends
+ * (:195, :269). */
+static void fano_block(const cco_code* c, int soft, float fw, const int32_t* fbm, const float* rx,
+                       const uint8_t* syms, cco_fano_node* nodes, uint8_t* out, int32_t* pm) {
+    const size_t T = cco_steps(c), OB = cco_out_bytes(c), NS = (size_t)1 << c->n;
+    const uint8_t mask = (uint8_t)((1u << c->n) - 1u);
+    const float fdelta = 17.0f;
+    const int32_t idelta = 17;
+    memset(nodes, 0, T * sizeof *nodes);
+    float fthr = 0.0f;
+    int32_t ithr = 0;
+    uint32_t timeout = CCO_FANO_TIMEOUT * (uint32_t)T;
+    size_t cur = 0, frontier = 0;
+#define RX(i) (soft ? rx + (i) * NS : NULL)
+#define SY(i) (soft ? 0 : (uint8_t)(syms[i] & mask))
+    fano_node_metrics(c, soft, fw, fbm, RX(0), SY(0), &nodes[0]);
+    int done = 0;
+    while (timeout != 0) {
+        timeout--;
+        cco_fano_node* cn = &nodes[cur];
+        float fms = cn->fmetric + cn->ftm[cn->sel];
+        int32_t ims = cn->imetric + cn->itm[cn->sel];
+        if (soft ? (fms >= fthr) : (ims >= ithr)) {
+            if (soft) {   /* tightening (:190-195) */
+                if (cn->fmetric < (fthr + fdelta))
+                    while (fms >= fthr + fdelta) fthr += fdelta;
+            } else {
+                if (cn->imetric < (ithr + idelta))
+                    while (ims >= ithr + idelta) ithr += idelta;
+            }
+            ++cur;
+            if (cur == T) { done = 1; break; }
+            cco_fano_node* nn = &nodes[cur];
+            nn->state = cn->succ[cn->sel];
+            nn->fmetric = fms;
+            nn->imetric = ims;
+            nn->decoded = 0;
+            nn->sel = 0;
+            fano_node_metrics(c, soft, fw, fbm, RX(cur), SY(cur), nn);
+            if (cur > frontier) frontier = cur;
+        } else {
+            for (;;) {
+                int cant = cur == 0;
+                if (!cant) {
+                    cco_fano_node* pn = &nodes[cur - 1];
+                    cant = soft ? (pn->fmetric < fthr) : (pn->imetric < ithr);
+                }
+                if (cant) {   /* relax the threshold, restart from the best branch (:241-250) */
+                    if (soft) fthr -= fdelta; else ithr -= idelta;
+                    if (nodes[cur].sel != 0) {
+                        nodes[cur].sel = 0;
+                        nodes[cur].decoded ^= 1;
+                    }
+                    break;
+                }
+                --cur;   /* move back (:251-261) */
+                if (nodes[cur].sel == 0) {
+                    nodes[cur].sel = 1;
+                    nodes[cur].decoded ^= 1;
+                    break;
+                }
+            }
+        }
+    }
+#undef RX
+#undef SY
+    if (pm) *pm = done ? nodes[T - 1].imetric : nodes[frontier].imetric;
+    memset(out, 0, OB);
+    for (size_t i = 0; i < T; ++i)
+        if (nodes[i].decoded == 1) out[i / 8] |= (uint8_t)(1u << (7 - i % 8));
+}
+
+void cco_fano_soft(const cco_code* c, float fano_metric_weight, const float* rx, size_t nblocks,
+                   uint8_t* out) {
+    size_t T = cco_steps(c), NS = (size_t)1 << c->n, OB = cco_out_bytes(c);
+    cco_fano_node* nodes = (cco_fano_node*)calloc(T, sizeof *nodes);
+    for (size_t b = 0; b < nblocks; ++b)
+        fano_block(c, 1, fano_metric_weight, NULL, rx + b * T * NS, NULL, nodes, out + b * OB, NULL);
+    free(nodes);
+}
+
+void cco_fano_hard(const cco_code* c, const int32_t* fano_bit_metrics, const uint8_t* syms,
+                   size_t nblocks, uint8_t* out, int32_t* path_metric) {
+    size_t T = cco_steps(c), OB = cco_out_bytes(c);
+    cco_fano_node* nodes = (cco_fano_node*)calloc(T, sizeof *nodes);
+    for (size_t b = 0; b < nblocks; ++b)
+        fano_block(c, 0, 0.0f, fano_bit_metrics, NULL, syms + b * T, nodes, out + b * OB,
+                   path_metric ? path_metric + b : NULL);
+    free(nodes);
+}
+
 /* AWGN-channel/main.c:129-141: compare the first blen bits, MSB-first. */
 uint64_t cco_count_errors(const cco_code* c, const uint8_t* info, const uint8_t* out, size_t nblocks) {
     size_t IB = cco_info_bytes(c), OB = cco_out_bytes(c);

@@ -85,6 +85,15 @@ int      cco_stack_soft(const cco_code* c, float metric_weight, const float* rx,
 int      cco_stack_hard(const cco_code* c, const int32_t* bit_metrics /* [2] */, const uint8_t* syms,
                         size_t nblocks, uint8_t* out, int32_t* path_metric /* [nb] */);
 
+/* Fano decoders, AWGN-channel/fano-decoder.c and binary-symmetric-channel/fano-decoder.c (KA9Q-
+ * derived threshold search, DELTA 17, timeout 10000 iterations per block bit). Soft branch metric
+ * (float)(1.0 + fano_metric_weight * d[sym]); hard: d * fano_bit_metrics[1] + (n - d) *
+ * fano_bit_metrics[0]. path_metric: the BSC decoder's callback metric. */
+void     cco_fano_soft(const cco_code* c, float fano_metric_weight, const float* rx, size_t nblocks,
+                       uint8_t* out);
+void     cco_fano_hard(const cco_code* c, const int32_t* fano_bit_metrics /* [2] */, const uint8_t* syms,
+                       size_t nblocks, uint8_t* out, int32_t* path_metric);
+
 /* Consumer: bit errors over the first blen bits of each block (AWGN-channel/main.c:118-144). */
 uint64_t cco_count_errors(const cco_code* c, const uint8_t* info, const uint8_t* out, size_t nblocks);
 

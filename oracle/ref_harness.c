@@ -12,7 +12,8 @@
  *   CODESPEC:     cb:<codebook index>  |  n:K:blen:poly0hex:poly1hex[:poly2hex]
  *   METRICS:      stack decoder metrics overriding the codebook's (code.h:14-16):
  *                 AWGN metric_weight (float) | BSC bit_metrics "m0,m1"
- * The same harness is linked against viterbi-decoder.c or stack-decoder.c (oracle/Makefile).
+ * The same harness is linked against viterbi-decoder.c, stack-decoder.c or fano-decoder.c
+ * (oracle/Makefile).
  * writes OUTPREFIX.info .rx .out [.pm] .meta
  */
 #include <stdint.h>
@@ -147,14 +148,15 @@ int main(int argc, char** argv) {
     harness_t h;
     memset(&h, 0, sizeof h);
     if (parse_code(argv[5], &h.param) != 0) { fprintf(stderr, "bad code spec\n"); return 2; }
+    /* METRICS overrides both the stack and the Fano fields (only one decoder is linked) */
 #ifdef HARNESS_AWGN
     h.scaling = (float)atof(argv[4]);
-    if (argc == 7) h.param.metric_weight = (float)atof(argv[6]);
+    if (argc == 7) h.param.metric_weight = h.param.fano_metric_weight = (float)atof(argv[6]);
 #else
     h.p_ppm = (int32_t)atol(argv[4]);
     if (argc == 7) {
         if (sscanf(argv[6], "%d,%d", &custom_bit_metrics[0], &custom_bit_metrics[1]) != 2) return 2;
-        h.param.bit_metrics = custom_bit_metrics;
+        h.param.bit_metrics = h.param.fano_bit_metrics = custom_bit_metrics;
     }
 #endif
     h.param.userdata = &h;
@@ -195,6 +197,10 @@ int main(int argc, char** argv) {
     for (int k = 0; k < h.param.symlen_out; ++k)
         fprintf(meta, "poly%d %016llx\n", k, (unsigned long long)h.param.polynomials[k]);
     fprintf(meta, "metric_weight %.9g\n", (double)h.param.metric_weight);
+    fprintf(meta, "fano_metric_weight %.9g\n", (double)h.param.fano_metric_weight);
+    fprintf(meta, "fano_bit_metric0 %d\nfano_bit_metric1 %d\n",
+            h.param.fano_bit_metrics ? h.param.fano_bit_metrics[0] : 0,
+            h.param.fano_bit_metrics ? h.param.fano_bit_metrics[1] : 0);
     fprintf(meta, "bit_metric0 %d\nbit_metric1 %d\n", h.param.bit_metrics ? h.param.bit_metrics[0] : 0,
             h.param.bit_metrics ? h.param.bit_metrics[1] : 0);
     fclose(meta);

@@ -29,7 +29,7 @@ typedef struct {
     int rc;
 } job_t;
 
-/* Stack-decoder builds (libccref_*_stack.so): code_param's stack metrics (code.h:14-16). */
+/* Stack / Fano builds (libccref_*_{stack,fano}.so): the sequential decoders' metrics (code.h:14-17). */
 static float g_metric_weight = -15.0f;
 static int32_t g_bit_metrics[2] = {1, -15};
 void ccref_set_stack_metrics(float metric_weight, int32_t bm0, int32_t bm1) {
@@ -62,8 +62,8 @@ static void* run_job(void* arg) {
     struct decoder* d = decoder_create();
     j->param.userdata = j;
     j->param.polynomials = j->polys;
-    j->param.metric_weight = g_metric_weight;
-    j->param.bit_metrics = g_bit_metrics;
+    j->param.metric_weight = j->param.fano_metric_weight = g_metric_weight;
+    j->param.bit_metrics = j->param.fano_bit_metrics = g_bit_metrics;
     if (!d || decoder_init(d, &j->param) != 0) { j->rc = -1; return NULL; }
     decoder_register_callback(d, on_decoded);
     const uint8_t* base = (const uint8_t*)j->in + j->first * j->steps * j->in_step_bytes;

@@ -16,7 +16,7 @@ def pytest_configure(config):
 
 
 def golden_manifest(kind="viterbi"):
-    name = "manifest.json" if kind == "viterbi" else "manifest_stack.json"
+    name = "manifest.json" if kind == "viterbi" else f"manifest_{kind}.json"
     with open(os.path.join(REPO, "tests", "golden", name)) as f:
         return json.load(f)
 

@@ -6,7 +6,7 @@ reference sources in place into oracle/_ref/ref_harness_{awgn,bsc} (driver logic
 and this script runs them with fixed seeds and packs what crossed the decoder boundary into one .npz
 per case (plain arrays, loaded with allow_pickle=False). The GPU box never runs this script.
 
-    python tests/golden/make_golden.py [--stack-only | --hd-only]
+    python tests/golden/make_golden.py [--stack-only | --hd-only | --fano-only]
 """
 import json
 import os
@@ -89,9 +89,25 @@ STACK_CASES = [
 ]
 
 
+# Fano-decoder cases (manifest_fano.json), same fields as STACK_CASES
+FANO_CASES = [
+    ("fano_awgn_cb0_4dB", "awgn", "cb:0", 601, 200, SCALING[4], None),
+    ("fano_awgn_cb0_8dB", "awgn", "cb:0", 602, 200, SCALING[8], None),
+    ("fano_awgn_cb3_4dB", "awgn", "cb:3", 603, 100, SCALING[4], None),
+    ("fano_awgn_cb4_6dB", "awgn", "cb:4", 604, 60, SCALING[6], None),
+    ("fano_awgn_cb5_4dB", "awgn", "cb:5", 605, 100, SCALING[4], None),
+    ("fano_awgn_k15_4dB", "awgn", K15.format(blen=40), 606, 100, SCALING[4], "-11.0"),
+    ("fano_awgn_k7_blen200_6dB", "awgn", K7.format(blen=200), 607, 20, SCALING[6], "-110.0"),
+    ("fano_bsc_cb0_p10000", "bsc", "cb:0", 701, 200, "10000", None),
+    ("fano_bsc_cb2_p30000", "bsc", "cb:2", 702, 100, "30000", None),
+    ("fano_bsc_cb4_p20000", "bsc", "cb:4", 703, 60, "20000", None),
+    ("fano_bsc_k15_p30000", "bsc", K15.format(blen=40), 704, 100, "30000", "1,-11"),
+]
+
+
 def run_case(name, channel, spec, seed, nblocks, param, tmp, decoder="viterbi", metrics=None,
              demapper="soft"):
-    suffix = ("_stack" if decoder == "stack" else "") + ("_hd" if demapper == "hard" else "")
+    suffix = ("" if decoder == "viterbi" else "_" + decoder) + ("_hd" if demapper == "hard" else "")
     exe = os.path.join(REF_DIR, f"ref_harness_{channel}{suffix}")
     prefix = os.path.join(tmp, name)
     cmd = [exe, prefix, str(seed), str(nblocks), param, spec] + ([metrics] if metrics else [])
@@ -121,11 +137,15 @@ def run_case(name, channel, spec, seed, nblocks, param, tmp, decoder="viterbi", 
     if decoder == "stack":
         arrays["metric_weight"] = np.float32(float(meta["metric_weight"]))
         arrays["bit_metrics"] = np.array([int(meta["bit_metric0"]), int(meta["bit_metric1"])], np.int32)
+    if decoder == "fano":
+        arrays["fano_metric_weight"] = np.float32(float(meta["fano_metric_weight"]))
+        arrays["fano_bit_metrics"] = np.array([int(meta["fano_bit_metric0"]), int(meta["fano_bit_metric1"])],
+                                              np.int32)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
     entry = {"name": name, "channel": channel, "spec": spec, "seed": seed, "nblocks": nblocks,
              "param": param, "errors": int(meta["errors"])}
-    if decoder == "stack":
-        entry.update(decoder="stack", metrics=metrics)
+    if decoder in ("stack", "fano"):
+        entry.update(decoder=decoder, metrics=metrics)
     if demapper == "hard":
         entry.update(demapper="hard")
     return entry
@@ -136,12 +156,12 @@ def main():
         sys.exit("make_golden.py needs /root/reference (build container only)")
     subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     manifest = []
-    only_new = "--stack-only" in sys.argv or "--hd-only" in sys.argv
+    only_new = any(a in sys.argv for a in ("--stack-only", "--hd-only", "--fano-only"))
     with tempfile.TemporaryDirectory() as tmp:
         for case in ([] if only_new else CASES):
             manifest.append(run_case(*case, tmp))
             print(manifest[-1])
-        if "--stack-only" not in sys.argv:
+        if "--stack-only" not in sys.argv and "--fano-only" not in sys.argv:
             if only_new:   # append to the existing manifest without rewriting the other fixtures
                 with open(os.path.join(HERE, "manifest.json")) as f:
                     manifest = [m for m in json.load(f) if m.get("demapper") != "hard"]
@@ -153,6 +173,16 @@ def main():
             json.dump(manifest, f, indent=1)
     if "--hd-only" in sys.argv:
         return
+    if "--fano-only" in sys.argv or "--stack-only" not in sys.argv:
+        fano = []
+        with tempfile.TemporaryDirectory() as tmp:
+            for name, channel, spec, seed, nb, param, metrics in FANO_CASES:
+                fano.append(run_case(name, channel, spec, seed, nb, param, tmp, "fano", metrics))
+                print(fano[-1])
+        with open(os.path.join(HERE, "manifest_fano.json"), "w") as f:
+            json.dump(fano, f, indent=1)
+        if "--fano-only" in sys.argv:
+            return
     stack = []
     with tempfile.TemporaryDirectory() as tmp:
         for name, channel, spec, seed, nb, param, metrics in STACK_CASES:

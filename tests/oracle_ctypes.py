@@ -58,6 +58,10 @@ def lib():
                                      ctypes.c_void_p]
         L.cco_stack_hard.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.cco_fano_soft.argtypes = [P(CcoCode), ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p]
+        L.cco_fano_hard.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p, ctypes.c_void_p]
         L.cco_count_errors.argtypes = [P(CcoCode), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         L.cco_count_errors.restype = ctypes.c_uint64
         _lib = L
@@ -140,6 +144,26 @@ def stack_hard(c, bit_metrics, syms):
     pm = np.zeros(syms.shape[0], np.int32)
     if lib().cco_stack_hard(ctypes.byref(c), _ptr(bm), _ptr(syms), syms.shape[0], _ptr(out), _ptr(pm)):
         raise RuntimeError("the reference would read past its buffers on some block")
+    return out, pm
+
+
+def fano_soft(c, fano_metric_weight, rx):
+    """Fano decoder restatement (AWGN-channel/fano-decoder.c)."""
+    rx = np.ascontiguousarray(rx, dtype=np.float32)
+    _, _, OB = dims(c)
+    out = np.zeros((rx.shape[0], OB), np.uint8)
+    lib().cco_fano_soft(ctypes.byref(c), float(fano_metric_weight), _ptr(rx), rx.shape[0], _ptr(out))
+    return out
+
+
+def fano_hard(c, fano_bit_metrics, syms):
+    """Fano decoder restatement (binary-symmetric-channel/fano-decoder.c); (out, path metric)."""
+    syms = np.ascontiguousarray(syms, dtype=np.uint8)
+    bm = np.ascontiguousarray(fano_bit_metrics, dtype=np.int32)
+    _, _, OB = dims(c)
+    out = np.zeros((syms.shape[0], OB), np.uint8)
+    pm = np.zeros(syms.shape[0], np.int32)
+    lib().cco_fano_hard(ctypes.byref(c), _ptr(bm), _ptr(syms), syms.shape[0], _ptr(out), _ptr(pm))
     return out, pm
 
 

@@ -1,0 +1,126 @@
+"""GPU parity of the Fano decoder (ccv_fano_plan_create / ccv_fano_decode_device,
+convolutional-codes_amd/csrc/fano_dev.hpp) against the unmodified reference fano-decoder.c outputs
+(tests/golden/fano_*.npz, manifest_fano.json: codebook codes 0, 2, 3, 4 (WSPR K=32), 5, K=15, a
+K=7 blen-200 case that runs into the timeout; AWGN and BSC) and the oracle restatement on seeded
+frames, plus the per-block search length export and the fused error count."""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from ccviterbi import (CODEBOOK, GEN_REF_X86, GEN_TRUE_PARITY, HARD, K15, SOFT, Code, FanoPlan,
+                       channel as ch)
+from conftest import golden_manifest
+
+pytestmark = pytest.mark.gpu
+FANO_CASES = golden_manifest("fano")
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+def _fano_code(g, gen=GEN_REF_X86):
+    return Code(int(g["n"]), int(g["K"]), int(g["blen"]), tuple(int(p) for p in g["polys"]), gen,
+                fano_bit_metrics=tuple(int(x) for x in g["fano_bit_metrics"]),
+                fano_metric_weight=float(g["fano_metric_weight"]))
+
+
+def _ocode(c: Code):
+    return O.code(c.n, c.K, c.blen, c.polys, c.gen_mode)
+
+
+@pytest.mark.parametrize("case", FANO_CASES, ids=[c["name"] for c in FANO_CASES])
+def test_fano_golden_fixture(case):
+    g = O.load_golden(case["name"])
+    c = _fano_code(g)
+    channel = SOFT if case["channel"] == "awgn" else HARD
+    plan = FanoPlan(c, channel)
+    assert plan.kernel == "fano"
+    res = plan.decode_host(g["rx"])
+    if channel == SOFT:
+        out = res
+    else:
+        out, pm = res
+        assert np.array_equal(pm, g["path_metric"])
+    assert np.array_equal(out, g["out"])
+    assert ch.count_bit_errors(c, g["info"], out) == int(g["errors"])
+
+
+SEEDED = [
+    ("code0_soft", CODEBOOK[0], SOFT), ("code0_hard", CODEBOOK[0], HARD),
+    ("code3_soft", CODEBOOK[3], SOFT), ("code5_soft", CODEBOOK[5], SOFT),
+    ("wspr_soft", CODEBOOK[4], SOFT), ("wspr_hard", CODEBOOK[4], HARD),
+    ("k15_soft", K15, SOFT), ("k15_true_soft", K15.with_(gen_mode=GEN_TRUE_PARITY), SOFT),
+    ("k15_hard", K15, HARD),
+]
+
+
+@pytest.mark.parametrize("name,c,channel", SEEDED, ids=[s[0] for s in SEEDED])
+def test_fano_seeded_vs_oracle(name, c, channel):
+    nb = 300
+    for db, p_ppm in ((4.0, 30000), (7.0, 8000)):
+        if channel == SOFT:
+            info, data = ch.awgn_blocks(c, nb, ch.noise_scaling(db), 31 + c.K)
+            ref = O.fano_soft(_ocode(c), c.fano_metric_weight, data)
+            assert np.array_equal(FanoPlan(c, SOFT).decode_host(data), ref)
+        else:
+            info, data = ch.bsc_blocks(c, nb, p_ppm, 41 + c.K)
+            ref, ref_pm = O.fano_hard(_ocode(c), c.fano_bit_metrics, data)
+            out, pm = FanoPlan(c, HARD).decode_host(data)
+            assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+
+
+def test_fano_timeouts_iterations_and_error_count(torch_cuda):
+    """A channel bad enough that some searches hit the reference's 10000*T timeout: outputs still
+    bit-exact, the exported search length shows the timeouts, the fused error count matches."""
+    torch = torch_cuda
+    c = CODEBOOK[0]
+    nb = 400
+    info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(1.5), 3)
+    ref = O.fano_soft(_ocode(c), c.fano_metric_weight, rx)
+    plan = FanoPlan(c, SOFT)
+    d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    d_it = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    plan.decode_fano_device(torch.from_numpy(rx).cuda(), nb, d_out, d_info=torch.from_numpy(info).cuda(),
+                            d_errors=d_err, d_iterations=d_it)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    assert np.array_equal(out, ref)
+    assert int(d_err.item()) == ch.count_bit_errors(c, info, out)
+    it = d_it.cpu().numpy().astype(np.int64)
+    assert (it >= c.steps).all()
+    assert (it <= 10000 * c.steps).all()
+    assert (it == 10000 * c.steps).any()          # some blocks timed out (the search gave up)
+    assert (it < 10000 * c.steps).any()
+
+
+def test_fano_plan_limits():
+    with pytest.raises(Exception, match="uint8_t"):
+        FanoPlan(K15.with_(blen=250), SOFT)           # T = 264 > 255
+
+
+@pytest.mark.parametrize("case", FANO_CASES, ids=[c["name"] for c in FANO_CASES])
+def test_reference_driver_with_mi355x_fano_decoder(case, tmp_path):
+    """Drop-in check: oracle/ref_harness.c (the reference drivers' producer chain and callbacks)
+    linked to libccv_fano_{awgn,bsc}.so instead of fano-decoder.c reproduces the reference's output
+    files byte for byte."""
+    import os
+    import subprocess
+    from conftest import REPO
+    exe = os.path.join(REPO, "oracle", "_ref", f"ref_harness_{case['channel']}_fano_ccv")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref drop-in harness not built (needs /root/reference at build time)")
+    g = O.load_golden(case["name"])
+    prefix = str(tmp_path / case["name"])
+    cmd = [exe, prefix, str(case["seed"]), str(case["nblocks"]), case["param"], case["spec"]]
+    subprocess.run(cmd + ([case["metrics"]] if case["metrics"] else []), check=True, timeout=300)
+    out = np.fromfile(prefix + ".out", dtype=np.uint8).reshape(g["out"].shape)
+    assert np.array_equal(out, g["out"])
+    if case["channel"] == "bsc":
+        assert np.array_equal(np.fromfile(prefix + ".pm", dtype=np.int32), g["path_metric"])
+    meta = dict(line.split() for line in open(prefix + ".meta"))
+    assert int(meta["errors"]) == case["errors"]

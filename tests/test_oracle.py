@@ -58,6 +58,23 @@ def test_stack_oracle_matches_reference_fixture(case):
     assert O.count_errors(c, g["info"], out) == int(g["errors"]) == case["errors"]
 
 
+FANO_CASES = golden_manifest("fano")
+
+
+@pytest.mark.parametrize("case", FANO_CASES, ids=[c["name"] for c in FANO_CASES])
+def test_fano_oracle_matches_reference_fixture(case):
+    """Fano restatement vs the unmodified reference fano-decoder.c (timeouts included)."""
+    g = O.load_golden(case["name"])
+    c = O.golden_code(g)
+    if case["channel"] == "awgn":
+        out = O.fano_soft(c, float(g["fano_metric_weight"]), g["rx"])
+    else:
+        out, pm = O.fano_hard(c, g["fano_bit_metrics"], g["rx"])
+        assert np.array_equal(pm, g["path_metric"])
+    assert np.array_equal(out, g["out"])
+    assert O.count_errors(c, g["info"], out) == int(g["errors"]) == case["errors"]
+
+
 def test_rand_restatement_matches_glibc():
     libc = ctypes.CDLL(ctypes.util.find_library("c"))
     for seed in (1, 2, 12345, 0xC0DE, 2**31 - 1):
