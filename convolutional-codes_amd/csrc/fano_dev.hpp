@@ -48,7 +48,9 @@ struct FanoArgs {
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
 constexpr int kFanoThreads = 64;
 
-template <bool HARD, int NP, bool W32>
+// RXL: the block's received symbols are copied into LDS ([t][k][lane]) when a lane takes the block,
+// taking global-memory latency off every search step (used when they fit, see launch_fano).
+template <bool HARD, int NP, bool W32, bool RXL>
 __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   using MT = typename std::conditional<HARD, int32_t, float>::type;
   using ET = typename std::conditional<HARD, uint8_t, float>::type;
@@ -58,6 +60,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   const int NS = HARD ? 1 : (1 << n);
   MT* metric = reinterpret_cast<MT*>(smem);                                    // [T][64]
   uint8_t* flags = smem + (size_t)T * kFanoThreads * sizeof(MT);              // [T][64]: sel | dec << 1
+  ET* rxl = reinterpret_cast<ET*>(smem + (size_t)T * kFanoThreads * (sizeof(MT) + 1));   // [T][NS][64]
   uint64_t poly[kMaxN];
 #pragma unroll
   for (int k = 0; k < kMaxN; ++k) poly[k] = a.poly[k];
@@ -71,6 +74,9 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     const unsigned int b = atomicAdd(a.next_block, 1u);
     if (b >= (unsigned int)a.nblocks) break;
     const ET* rx = in + (size_t)b * T * NS;
+    if constexpr (RXL) {
+      for (int i = 0; i < T * NS; ++i) rxl[i * kFanoThreads + lane] = rx[i];
+    }
     // get_transition_metric + sort (:160-181, :213-236) for the node at depth d with state st:
     // tm0 >= tm1 afterwards, swapped = input 1 is the best branch
     auto node_metrics = [&](int d, uint64_t st, MT& tm0, MT& tm1, uint32_t& swapped) {
@@ -78,14 +84,21 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       const uint32_t e0 = es >> 8, e1 = es & 0xFFu;
       MT t0, t1;
       if constexpr (HARD) {
-        const uint32_t r = rx[d] & symmask;
+        const uint32_t r = (RXL ? rxl[d * kFanoThreads + lane] : rx[d]) & symmask;
         const int32_t d0 = __builtin_popcount(e0 ^ r), d1 = __builtin_popcount(e1 ^ r);
         t0 = d0 * a.bm1 + (n - d0) * a.bm0;
         t1 = d1 * a.bm1 + (n - d1) * a.bm0;
       } else {
-        const ET* r = rx + (size_t)d * NS;
-        t0 = (float)(1.0 + (double)(a.weight * r[e0]));
-        t1 = (float)(1.0 + (double)(a.weight * r[e1]));
+        float r0, r1;
+        if constexpr (RXL) {
+          r0 = rxl[(d * NS + (int)e0) * kFanoThreads + lane];
+          r1 = rxl[(d * NS + (int)e1) * kFanoThreads + lane];
+        } else {
+          r0 = rx[(size_t)d * NS + e0];
+          r1 = rx[(size_t)d * NS + e1];
+        }
+        t0 = (float)(1.0 + (double)(a.weight * r0));
+        t1 = (float)(1.0 + (double)(a.weight * r1));
       }
       swapped = t0 < t1 ? 1u : 0u;
       tm0 = swapped ? t1 : t0;
