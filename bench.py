@@ -44,13 +44,13 @@ def cpu_threads():
     return max(1, min(16, n))
 
 
-def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi"):
+def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi", hard=False):
     """Reference decoder (oracle/_ref, compiled from the reference's own sources) on host cores,
     over a bounded sample of the SAME frames the GPU decodes; its output is checked against the GPU's.
     Falls back to the oracle restatement ("port", one thread) where oracle/_ref was not built."""
     stack = decoder == "stack"
     suffix = "" if decoder == "viterbi" else "_" + decoder
-    ref_so = os.path.join(REPO, "oracle", "_ref", f"libccref_awgn{suffix}.so")
+    ref_so = os.path.join(REPO, "oracle", "_ref", f"libccref_{'bsc' if hard else 'awgn'}{suffix}.so")
     polys = (ctypes.c_uint64 * code.n)(*code.polys)
     if os.path.exists(ref_so):
         lib = ctypes.CDLL(ref_so)
@@ -83,7 +83,12 @@ def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi"):
 
         def run(nb, nthr):
             t0 = time.perf_counter()
-            if decoder == "stack":
+            if hard:
+                fn = {"stack": lambda: O.stack_hard(oc, code.bit_metrics, rx[:nb]),
+                      "fano": lambda: O.fano_hard(oc, code.fano_bit_metrics, rx[:nb])}.get(
+                          decoder, lambda: O.viterbi_hard(oc, rx[:nb]))
+                out = fn()[0]
+            elif decoder == "stack":
                 out = O.stack_soft(oc, code.metric_weight, rx[:nb])
             elif decoder == "fano":
                 out = O.fano_soft(oc, code.fano_metric_weight, rx[:nb])
@@ -141,6 +146,9 @@ def main():
                     help="1 M-bit frames per GPU per step (64 = 1.6 M blocks = 25,000 one-wave tiles, "
                          "~6 waves per SIMD so the last partial round is a small fraction)")
     ap.add_argument("--ebn0", type=float, default=4.0)
+    ap.add_argument("--channel", choices=("awgn", "bsc"), default="awgn",
+                    help="awgn: soft decision (configs 2, 3, 5); bsc: hard decision (configs 1, 4)")
+    ap.add_argument("--p-ppm", type=int, default=50000, help="BSC crossover probability in ppm")
     ap.add_argument("--layout", choices=("block", "step"), default="block",
                     help="input layout in HBM: block-major [nb][T][4] as the reference decoder consumes "
                          "it, or step-major [T][nb][4] (CCV_FLAG_STEP_MAJOR)")
@@ -154,7 +162,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from ccviterbi import SOFT, FanoPlan, Plan, StackPlan, channel as ch, named_code
+    from ccviterbi import HARD, SOFT, FanoPlan, Plan, StackPlan, channel as ch, named_code
     from ccviterbi.decoder import FLAG_STEP_MAJOR
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,19 +183,27 @@ def main():
     code = named_code(args.code)
     nb = args.frames * FRAME_BLOCKS
     # this rank's frames: blocks [rank*nb, (rank+1)*nb) of the Philox stream
-    info, rx = ch.awgn_blocks(code, nb, ch.noise_scaling(args.ebn0), args.seed, first_block=rank * nb,
-                              threads=cpu_threads())
+    hard = args.channel == "bsc"
+    if hard and args.layout != "block":
+        raise SystemExit("hard-decision input is one byte per step, block-major")
+    chan = HARD if hard else SOFT
+    if hard:
+        info, rx = ch.bsc_blocks(code, nb, args.p_ppm, args.seed, first_block=rank * nb,
+                                 threads=cpu_threads())
+    else:
+        info, rx = ch.awgn_blocks(code, nb, ch.noise_scaling(args.ebn0), args.seed, first_block=rank * nb,
+                                  threads=cpu_threads())
     host_in = rx if args.layout == "block" else np.ascontiguousarray(rx.transpose(1, 0, 2))
     d_rx = torch.from_numpy(host_in).to("cuda")
     d_info = torch.from_numpy(info).to("cuda")
     d_out = torch.empty((nb, code.out_bytes), dtype=torch.uint8, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
     if args.decoder == "stack":
-        plan = StackPlan(code, SOFT)
+        plan = StackPlan(code, chan)
     elif args.decoder == "fano":
-        plan = FanoPlan(code, SOFT)
+        plan = FanoPlan(code, chan)
     else:
-        plan = Plan(code, SOFT, FLAG_STEP_MAJOR if args.layout == "step" else 0)
+        plan = Plan(code, chan, FLAG_STEP_MAJOR if args.layout == "step" else 0)
     plan.reserve(nb)
     stream = torch.cuda.current_stream()
 
@@ -236,7 +252,7 @@ def main():
     fused = None
     if rank == 0 and not args.no_fused_channel and not sequential:
         d_ferr = torch.zeros(1, dtype=torch.int64, device="cuda")
-        scaling = ch.noise_scaling(args.ebn0)
+        scaling = args.p_ppm if hard else ch.noise_scaling(args.ebn0)
         plan.simulate_device(args.seed, 0, nb, scaling, d_errors=d_ferr, stream=stream)   # warm-up
         d_ferr.zero_()
         reps = 5
@@ -262,14 +278,15 @@ def main():
     errors = int(errs.item())
 
     if rank == 0:
-        bpb = algorithmic_bytes_per_bit(code, decisions=not sequential)
+        bpb = algorithmic_bytes_per_bit(code, soft=not hard, decisions=not sequential)
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-        workload_key = f"{args.code}:frames{args.frames}:{args.layout}"
+        workload_key = f"{args.code}:frames{args.frames}:{args.layout}" + (":bsc" if hard else "")
         traffic = load_pmc_traffic(workload_key)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, _ = cpu_baseline(code, rx, d_out.cpu().numpy(), args.cpu_seconds, decoder=args.decoder)
+            cpu, _ = cpu_baseline(code, rx, d_out.cpu().numpy(), args.cpu_seconds, decoder=args.decoder,
+                                  hard=hard)
         line = {
             "metric": METRIC,
             "value": round(bits_per_step * args.steps / wall / 1e6, 2),
@@ -281,11 +298,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic: Philox AWGN channel at the reference's noise scaling, host-demapped, "
-                    "resident in HBM before timing",
+            "dtype": "u16" if hard else "f32",
+            "data": ("synthetic: Philox BSC channel (per-bit flips at p_ppm), resident in HBM before timing"
+                     if hard else
+                     "synthetic: Philox AWGN channel at the reference's noise scaling, host-demapped, "
+                     "resident in HBM before timing"),
             "config": {
-                "workload": f"awgn-simulation {code.name or args.code} r=1/{code.n} K={code.K} soft "
+                "workload": f"{'binary-symmetric' if hard else 'awgn'}-simulation {code.name or args.code} "
+                            f"r=1/{code.n} K={code.K} {'hard' if hard else 'soft'} "
                             f"{ {'stack': 'stack decoder', 'fano': 'Fano decoder'}.get(args.decoder, 'Viterbi')}, "
                             f"blen {code.blen}, "
                             f"{args.frames} x 1M-bit frames per GPU per step",
@@ -293,13 +313,16 @@ def main():
                 "generator": "ref-x86" if code.gen_mode == 0 else "true-parity",
                 "frames_per_gpu_per_step": args.frames,
                 "blocks_per_gpu_per_step": nb,
-                "ebn0_db": args.ebn0,
+                "channel": args.channel,
+                **({"p_ppm": args.p_ppm} if hard else {"ebn0_db": args.ebn0}),
                 "parallelism": f"dp{world} (frames sharded, counters all-reduced once)",
                 "kernel": plan.kernel,
-                "input_layout": "block-major [nb][T][2^n] (reference)" if args.layout == "block"
-                                else "step-major [T][nb][2^n]",
+                "input_layout": ("block-major [nb][T] symbols (reference)" if hard else
+                                 "block-major [nb][T][2^n] (reference)" if args.layout == "block"
+                                 else "step-major [T][nb][2^n]"),
             },
-            "ber": {"ebn0_db": args.ebn0, "errors": errors, "bits": bits_per_step * args.steps,
+            "ber": {**({"p_ppm": args.p_ppm} if hard else {"ebn0_db": args.ebn0}),
+                    "errors": errors, "bits": bits_per_step * args.steps,
                     "ber": errors / (bits_per_step * args.steps)},
             "kernel_ms": round(kernel_ms, 4),
             "pcie_inclusive_mbit_s": round(nb * code.blen / pcie_s / 1e6, 1) if pcie_s else None,

@@ -39,6 +39,25 @@ __device__ __forceinline__ float vmin(float a, float b) {
   return r;
 }
 __device__ __forceinline__ uint32_t vmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// 16-bit metrics (the BSC reference keeps uint16_t ones): v_add_u16 / v_min_u16 issue at full rate on
+// gfx950 where v_min_u32 is half rate (profiles/r01_rates_packed16.txt). H16 holds the metric in
+// the low half of a VGPR (high half don't-care); the ops are pinned by inline asm because hipcc
+// otherwise folds the branch-metric popcounts into every add (v_bcnt, half rate) and turns the
+// decision into compare + select. v_add_u16 / v_min_u16 zero the high half (measured: tools/t16), so
+// every metric stays zero-extended and the decision is the sign of the full-rate 32-bit m1 - m0.
+struct H16 {
+  uint32_t v;
+};
+__device__ __forceinline__ H16 operator+(H16 a, H16 b) {
+  H16 r;
+  asm("v_add_u16_e32 %0, %1, %2" : "=v"(r.v) : "v"(a.v), "v"(b.v));
+  return r;
+}
+__device__ __forceinline__ H16 vmin(H16 a, H16 b) {
+  H16 r;
+  asm("v_min_u16_e32 %0, %1, %2" : "=v"(r.v) : "v"(a.v), "v"(b.v));
+  return r;
+}
 
 // shift the decision (m1 < m0) into d: sign bit of m1 - m0 (exact for finite fp32 and for
 // finite-vs-inf; inf-inf only occurs at states no traceback can reach).
@@ -47,6 +66,11 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t d, float m0, float m1) {
 }
 __device__ __forceinline__ uint32_t shift_in(uint32_t d, uint32_t m0, uint32_t m1) {
   return (d << 1) | ((m1 - m0) >> 31);
+}
+__device__ __forceinline__ uint32_t shift_in(uint32_t d, H16 m0, H16 m1) {
+  uint32_t diff;
+  asm("v_sub_u32_e32 %0, %1, %2" : "=v"(diff) : "v"(m1.v), "v"(m0.v));
+  return __builtin_amdgcn_alignbit(d, diff, 31);
 }
 
 template <int NS>
@@ -403,12 +427,21 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_hard_reg(RegArgs a) {
     branch_metrics(p[t], BM);
     dec[(size_t)t * dstride] = acs_step<C, true, uint32_t>(M, BM);
   }
+  // afterwards every metric is <= n*T < 2^15: the ACS runs on 16-bit metrics, exactly the
+  // reference's uint16_t arithmetic
+  H16 M16[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) M16[s].v = M[s];
   pipelined_steps<kHardPF, uint32_t>(t0, T, [&](int t) { return (uint32_t)p[t]; },
                                      [&](uint32_t sym, int t) {
-                                       uint32_t BM[NS];
-                                       branch_metrics(sym, BM);
-                                       dec[(size_t)t * dstride] = acs_step<C, false, uint32_t>(M, BM);
+                                       H16 BM[NS];
+#pragma unroll
+                                       for (int k = 0; k < NS; ++k)
+                                         BM[k].v = (uint32_t)__builtin_popcount((uint32_t)k ^ (sym & kMask));
+                                       dec[(size_t)t * dstride] = acs_step<C, false, H16>(M16, BM);
                                      });
+#pragma unroll
+  for (int s = 0; s < S; ++s) M[s] = M16[s].v & 0xFFFFu;
   uint32_t errors = 0;
   if (b < nb) {
     uint32_t best;
