@@ -48,134 +48,145 @@ struct FanoArgs {
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
 constexpr int kFanoThreads = 64;
 
-// RXL: the block's received symbols are copied into LDS ([t][k][lane]) when a lane takes the block,
-// taking global-memory latency off every search step (used when they fit, see launch_fano).
-template <bool HARD, int NP, bool W32, bool RXL>
+// Received-symbol storage per lane:
+//   ROWS (hard input, or soft rate-1/2): the block's symbols are copied into LDS when a lane takes
+//   the block, one row per node ([T][64] bytes / float4s), and each search step prefetches the rows
+//   of the two nodes it can move to (cur - 1, cur + 1) while the lane keeps its own node's row in
+//   registers: no memory latency after the move is decided.
+//   otherwise: branch metrics read r[e] straight from the block in global memory.
+template <bool HARD, int NP>
+struct FanoRow;
+template <int NP>
+struct FanoRow<true, NP> {
+  uint32_t v;
+  // component-wise select: a select of whole structs becomes a private-memory copy
+  __device__ void pick(bool a, const FanoRow& ra, bool b, const FanoRow& rb) {
+    v = a ? ra.v : (b ? rb.v : v);
+  }
+};
+template <int NP>
+struct FanoRow<false, NP> {
+  float4 v;
+  __device__ void pick(bool a, const FanoRow& ra, bool b, const FanoRow& rb) {
+    v.x = a ? ra.v.x : (b ? rb.v.x : v.x);
+    v.y = a ? ra.v.y : (b ? rb.v.y : v.y);
+    v.z = a ? ra.v.z : (b ? rb.v.z : v.z);
+    v.w = a ? ra.v.w : (b ? rb.v.w : v.w);
+  }
+};
+
+// One lane, one search. The reference's loop (:183-263) is an outer iteration (one timeout tick:
+// try the selected branch, move forward or start looking back) with an inner loop of backward moves.
+// Here every pass of the kernel loop is ONE move -- forward, one step back, or a threshold
+// relaxation -- so all lanes of a wave stay in the same code whatever phase their searches are in,
+// and the branch metrics of the node a lane lands on are computed by one shared piece of code.
+template <bool HARD, int NP, bool W32, bool ROWS>
 __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   using MT = typename std::conditional<HARD, int32_t, float>::type;
   using ET = typename std::conditional<HARD, uint8_t, float>::type;
+  using ST = typename std::conditional<W32, uint32_t, uint64_t>::type;
+  static_assert(!ROWS || HARD || NP == 2, "rows of received symbols are a byte or a float4");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const int T = a.T, K = a.K, n = a.n;
   const int NS = HARD ? 1 : (1 << n);
-  MT* metric = reinterpret_cast<MT*>(smem);                                    // [T][64]
-  uint8_t* flags = smem + (size_t)T * kFanoThreads * sizeof(MT);              // [T][64]: sel | dec << 1
-  ET* rxl = reinterpret_cast<ET*>(smem + (size_t)T * kFanoThreads * (sizeof(MT) + 1));   // [T][NS][64]
+  // node arrays [T + 1][64]; row T takes the stores a lane does not need
+  MT* metric = reinterpret_cast<MT*>(smem);
+  uint8_t* flags = smem + (size_t)(T + 1) * kFanoThreads * sizeof(MT);   // sel | dec << 1
+  // rows: [T][64] float4 (soft) or bytes (hard), after the flags (16-byte aligned)
+  unsigned char* rows = smem + (((size_t)(T + 1) * kFanoThreads * (sizeof(MT) + 1) + 15) & ~(size_t)15);
   uint64_t poly[kMaxN];
 #pragma unroll
   for (int k = 0; k < kMaxN; ++k) poly[k] = a.poly[k];
   const bool idiom = a.gen == GEN_REF_X86;
   const MT delta = (MT)17;                                                     // fano-decoder.c:15
-  const uint64_t smask = (1ull << (K - 1)) - 1ull;   // K <= 64
-  const uint8_t symmask = (uint8_t)((1u << n) - 1u);
+  const ST smask = (ST)((1ull << (K - 1)) - 1ull);   // K <= 64
+  const uint32_t symmask = (1u << n) - 1u;
   const ET* in = reinterpret_cast<const ET*>(a.in);
+  const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+  const uint32_t budget = (uint32_t)kFanoTimeoutPerBit * (uint32_t)T;
 
-  for (;;) {
-    const unsigned int b = atomicAdd(a.next_block, 1u);
-    if (b >= (unsigned int)a.nblocks) break;
-    const ET* rx = in + (size_t)b * T * NS;
-    if constexpr (RXL) {
-      for (int i = 0; i < T * NS; ++i) rxl[i * kFanoThreads + lane] = rx[i];
+  auto row_at = [&](int d) {
+    FanoRow<HARD, NP> r;
+    if constexpr (HARD) r.v = rows[d * kFanoThreads + lane];
+    else r.v = reinterpret_cast<const float4*>(rows)[d * kFanoThreads + lane];
+    return r;
+  };
+  // get_transition_metric + sort (:160-181, :213-236) for the node at depth d with state st, whose
+  // received row is `row` (ROWS): tm0 >= tm1 afterwards, swapped = input 1 is the best branch
+  auto node_metrics = [&](const ET* rx, int d, ST st, const FanoRow<HARD, NP>& row, MT& tm0, MT& tm1,
+                          uint32_t& swapped) {
+    const uint32_t es = lane_symbols<NP, W32>(poly, n, K, idiom, (uint64_t)st);
+    const uint32_t e0 = es >> 8, e1 = es & 0xFFu;
+    MT t0, t1;
+    if constexpr (HARD) {
+      const uint32_t r = (ROWS ? row.v : (uint32_t)rx[d]) & symmask;
+      const int32_t d0 = __builtin_popcount(e0 ^ r), d1 = __builtin_popcount(e1 ^ r);
+      t0 = d0 * a.bm1 + (n - d0) * a.bm0;
+      t1 = d1 * a.bm1 + (n - d1) * a.bm0;
+    } else {
+      float r0, r1;
+      if constexpr (ROWS) {
+        const float4 v = row.v;
+        r0 = (e0 & 2u) ? ((e0 & 1u) ? v.w : v.z) : ((e0 & 1u) ? v.y : v.x);
+        r1 = (e1 & 2u) ? ((e1 & 1u) ? v.w : v.z) : ((e1 & 1u) ? v.y : v.x);
+      } else {
+        r0 = rx[(size_t)d * NS + e0];
+        r1 = rx[(size_t)d * NS + e1];
+      }
+      t0 = (float)(1.0 + (double)(a.weight * r0));
+      t1 = (float)(1.0 + (double)(a.weight * r1));
     }
-    // get_transition_metric + sort (:160-181, :213-236) for the node at depth d with state st:
-    // tm0 >= tm1 afterwards, swapped = input 1 is the best branch
-    auto node_metrics = [&](int d, uint64_t st, MT& tm0, MT& tm1, uint32_t& swapped) {
-      const uint32_t es = lane_symbols<NP, W32>(poly, n, K, idiom, st);
-      const uint32_t e0 = es >> 8, e1 = es & 0xFFu;
-      MT t0, t1;
+    swapped = t0 < t1 ? 1u : 0u;
+    tm0 = swapped ? t1 : t0;
+    tm1 = swapped ? t0 : t1;
+  };
+
+  // per-lane search state
+  unsigned int b = atomicAdd(a.next_block, 1u);
+  const ET* rx = nullptr;
+  int cur = 0, frontier = 0;
+  ST st = 0;
+  MT mcur = 0, thr = 0, tm0 = 0, tm1 = 0;
+  uint32_t sel = 0, dec = 0, timeout = 0;
+  bool inback = false, moved = false;
+  FanoRow<HARD, NP> row0{};   // received row of node cur
+  // start a search (:108-124 reset, then the root's branch metrics)
+  auto start = [&]() {
+    rx = in + (size_t)b * T * NS;
+    if constexpr (ROWS) {
       if constexpr (HARD) {
-        const uint32_t r = (RXL ? rxl[d * kFanoThreads + lane] : rx[d]) & symmask;
-        const int32_t d0 = __builtin_popcount(e0 ^ r), d1 = __builtin_popcount(e1 ^ r);
-        t0 = d0 * a.bm1 + (n - d0) * a.bm0;
-        t1 = d1 * a.bm1 + (n - d1) * a.bm0;
+        for (int d = 0; d < T; ++d) rows[d * kFanoThreads + lane] = rx[d];
       } else {
-        float r0, r1;
-        if constexpr (RXL) {
-          r0 = rxl[(d * NS + (int)e0) * kFanoThreads + lane];
-          r1 = rxl[(d * NS + (int)e1) * kFanoThreads + lane];
-        } else {
-          r0 = rx[(size_t)d * NS + e0];
-          r1 = rx[(size_t)d * NS + e1];
-        }
-        t0 = (float)(1.0 + (double)(a.weight * r0));
-        t1 = (float)(1.0 + (double)(a.weight * r1));
+        const float4* src = reinterpret_cast<const float4*>(rx);
+        float4* dst = reinterpret_cast<float4*>(rows);
+        for (int d = 0; d < T; ++d) dst[d * kFanoThreads + lane] = src[d];
       }
-      swapped = t0 < t1 ? 1u : 0u;
-      tm0 = swapped ? t1 : t0;
-      tm1 = swapped ? t0 : t1;
-    };
-    for (int d = 0; d < T; ++d) flags[d * kFanoThreads + lane] = 0;   // reset (:108-124)
-    metric[lane] = (MT)0;
-    int cur = 0, frontier = 0;
-    uint64_t st = 0;            // state of node cur
-    MT mcur = 0, thr = 0;
-    MT tm0, tm1;
-    uint32_t swapped;
-    node_metrics(0, 0, tm0, tm1, swapped);
-    uint32_t sel = 0, dec = swapped;
-    flags[lane] = (uint8_t)(dec << 1);
-    uint32_t timeout = (uint32_t)kFanoTimeoutPerBit * (uint32_t)T;
-    bool done = false;
-    while (timeout != 0) {
-      --timeout;
-      const MT ms = mcur + (sel ? tm1 : tm0);
-      if (ms >= thr) {
-        if (mcur < thr + delta) {   // tightening (:190-195)
-          while (ms >= thr + delta) thr += delta;
-        }
-        // move forward along the selected branch (input = dec)
-        st = (st >> 1) | ((uint64_t)dec << (K - 2));
-        ++cur;
-        if (cur == T) { done = true; break; }
-        mcur = ms;
-        metric[cur * kFanoThreads + lane] = ms;
-        node_metrics(cur, st, tm0, tm1, swapped);
-        sel = 0;
-        dec = swapped;
-        flags[cur * kFanoThreads + lane] = (uint8_t)(dec << 1);
-        frontier = cur > frontier ? cur : frontier;
-      } else {
-        bool moved = false;
-        for (;;) {
-          const bool cant = cur == 0 || metric[(cur - 1) * kFanoThreads + lane] < thr;
-          if (cant) {   // relax the threshold, restart from the best branch (:241-250)
-            thr -= delta;
-            if (sel != 0) {
-              sel = 0;
-              dec ^= 1u;
-              flags[cur * kFanoThreads + lane] = (uint8_t)(dec << 1);
-            }
-            break;
-          }
-          // move back (:251-261): the state loses the input of node cur-1, regains that of cur-K
-          const uint32_t old = cur >= K ? (flags[(cur - K) * kFanoThreads + lane] >> 1) : 0u;
-          st = ((st << 1) & smask) | old;
-          --cur;
-          moved = true;
-          const uint32_t f = flags[cur * kFanoThreads + lane];
-          sel = f & 1u;
-          dec = f >> 1;
-          if (sel == 0) {
-            sel = 1;
-            dec ^= 1u;
-            flags[cur * kFanoThreads + lane] = (uint8_t)(1u | (dec << 1));
-            break;
-          }
-        }
-        if (moved) {
-          mcur = metric[cur * kFanoThreads + lane];
-          node_metrics(cur, st, tm0, tm1, swapped);
-        }
-      }
+      row0 = row_at(0);
     }
-    // output_data (:315-325): the decoded input of every node, MSB-first
-    const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+    metric[lane] = (MT)0;
+    cur = 0;
+    frontier = 0;
+    st = 0;
+    mcur = 0;
+    thr = 0;
+    uint32_t sw;
+    node_metrics(rx, 0, 0, row0, tm0, tm1, sw);
+    sel = 0;
+    dec = sw;
+    flags[lane] = (uint8_t)(dec << 1);
+    timeout = budget;
+    inback = false;
+  };
+  // output_data (:315-325): the decoded input of every node, MSB-first; nodes past the frontier
+  // were never visited and still hold the reset value 0
+  auto finish = [&](bool done) {
     uint32_t errors = 0;
     for (int j = 0; j < OB; ++j) {
       uint32_t byte = 0;
       for (int k = 0; k < 8; ++k) {
         const int d = 8 * j + k;
-        if (d < T) byte |= (uint32_t)(flags[d * kFanoThreads + lane] >> 1) << (7 - k);
+        if (d <= frontier && d < T) byte |= (uint32_t)(flags[d * kFanoThreads + lane] >> 1) << (7 - k);
       }
       a.out[(size_t)b * OB + j] = (uint8_t)byte;
       if (a.info && j < IB) {
@@ -187,10 +198,78 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     }
     if (a.err && errors) atomicAdd(a.err, (unsigned long long)errors);
     if constexpr (HARD) {
-      if (a.path_metric)
-        a.path_metric[b] = done ? metric[(T - 1) * kFanoThreads + lane] : metric[frontier * kFanoThreads + lane];
+      // the metric of the newest received node (:195, :269): the last node when done
+      if (a.path_metric) a.path_metric[b] = metric[(done ? T - 1 : frontier) * kFanoThreads + lane];
     }
-    if (a.iterations) a.iterations[b] = (uint32_t)kFanoTimeoutPerBit * (uint32_t)T - timeout;
+    if (a.iterations) a.iterations[b] = budget - timeout;
+  };
+
+  if (b >= (unsigned int)a.nblocks) return;
+  start();
+  // One move per pass, computed without branches (a lone lane's search is latency-bound and every
+  // taken branch costs the wave an instruction-fetch bubble); stores that a lane does not need go
+  // to the spare node row T.
+  for (;;) {
+    // everything a backward move can read, fetched before the move is decided
+    const int cm = cur > 0 ? cur - 1 : 0;
+    const MT mprev = metric[cm * kFanoThreads + lane];
+    const uint32_t fprev = flags[cm * kFanoThreads + lane];
+    const uint32_t fold = flags[(cur >= K ? cur - K : 0) * kFanoThreads + lane];
+    FanoRow<HARD, NP> rowm{}, rowp{};
+    if constexpr (ROWS) {
+      rowm = row_at(cm);
+      rowp = row_at(cur + 1 < T ? cur + 1 : T - 1);
+    }
+    // outer iteration (:183-196): one timeout tick, try the selected branch
+    const bool outer = !inback;
+    const bool expired = outer && timeout == 0;
+    const bool tick = outer && timeout != 0;
+    timeout -= tick ? 1u : 0u;
+    const MT ms = mcur + (sel ? tm1 : tm0);
+    const bool fwd = tick && ms >= thr;
+    if (fwd && mcur < thr + delta) {   // tightening (:190-195)
+      while (ms >= thr + delta) thr += delta;
+    }
+    // look back (:237-263): one step per pass
+    const bool entering = tick && !fwd;
+    const bool was_moved = entering ? false : moved;
+    const bool looking = entering || inback;
+    const bool cant = cur == 0 || mprev < thr;
+    const bool relax = looking && cant;   // relax the threshold, restart from the best branch
+    const bool bstep = looking && !cant;  // move back to node cur-1
+    const bool untried = (fprev & 1u) == 0u;   // node cur-1 has not tried its second branch yet
+    thr = relax ? thr - delta : thr;
+    const ST st_f = (ST)((st >> 1) | ((ST)dec << (K - 2)));
+    const ST st_b = (ST)(((st << 1) & smask) | (ST)(cur >= K ? (fold >> 1) : 0u));
+    st = fwd ? st_f : (bstep ? st_b : st);
+    const int ncur = cur + (fwd ? 1 : 0) - (bstep ? 1 : 0);
+    const bool flip = relax && sel != 0;
+    // sel/dec of the node the lane is on afterwards (forward: dec set from its branch metrics below)
+    dec = bstep ? ((fprev >> 1) ^ (untried ? 1u : 0u)) : (dec ^ (flip ? 1u : 0u));
+    sel = bstep ? 1u : ((fwd || relax) ? 0u : sel);
+    mcur = fwd ? ms : (bstep ? mprev : mcur);
+    inback = bstep && !untried;
+    moved = bstep || was_moved;
+    const bool need = fwd || (relax && was_moved) || (bstep && untried);
+    frontier = fwd && ncur > frontier ? ncur : frontier;
+    cur = ncur;
+    if (__builtin_expect(expired || (fwd && ncur == T), 0)) {
+      finish(!expired);
+      b = atomicAdd(a.next_block, 1u);
+      if (b >= (unsigned int)a.nblocks) break;
+      start();
+      continue;
+    }
+    metric[(fwd ? ncur : T) * kFanoThreads + lane] = ms;
+    if constexpr (ROWS) row0.pick(fwd, rowp, bstep, rowm);
+    MT n0, n1;
+    uint32_t sw;
+    node_metrics(rx, ncur, st, row0, n0, n1, sw);
+    tm0 = need ? n0 : tm0;
+    tm1 = need ? n1 : tm1;
+    dec = fwd ? sw : dec;
+    const bool wflag = fwd || flip || (bstep && untried);
+    flags[(wflag ? ncur : T) * kFanoThreads + lane] = (uint8_t)((bstep ? 1u : 0u) | (dec << 1));
   }
 }
 

@@ -40,42 +40,49 @@ hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
   return launch_pw<false, 10>(a, lds, s);
 }
 
-template <bool HARD, int NP, bool W32, bool RXL>
+template <bool HARD, int NP, bool W32, bool ROWS>
 static hipError_t launch_fano_v(const FanoArgs& a, int grid, size_t lds, hipStream_t s) {
-  const void* fn = reinterpret_cast<const void*>(&fano_decode<HARD, NP, W32, RXL>);
+  const void* fn = reinterpret_cast<const void*>(&fano_decode<HARD, NP, W32, ROWS>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((fano_decode<HARD, NP, W32, RXL>), dim3(grid), dim3(kFanoThreads), lds, s, a);
+  hipLaunchKernelGGL((fano_decode<HARD, NP, W32, ROWS>), dim3(grid), dim3(kFanoThreads), lds, s, a);
   return hipGetLastError();
 }
 
-template <bool HARD, bool RXL>
-static hipError_t launch_fano_h(const FanoArgs& a, int grid, size_t lds, hipStream_t s) {
+template <bool HARD>
+static hipError_t launch_fano_h(const FanoArgs& a, bool rows, int grid, size_t lds, hipStream_t s) {
   if (a.K <= 32) {
-    if (a.n == 2) return launch_fano_v<HARD, 2, true, RXL>(a, grid, lds, s);
-    if (a.n == 3) return launch_fano_v<HARD, 3, true, RXL>(a, grid, lds, s);
+    if (a.n == 2)
+      return rows ? launch_fano_v<HARD, 2, true, true>(a, grid, lds, s)
+                  : launch_fano_v<HARD, 2, true, false>(a, grid, lds, s);
+    if (a.n == 3)
+      return (HARD && rows) ? launch_fano_v<HARD, 3, true, HARD>(a, grid, lds, s)
+                            : launch_fano_v<HARD, 3, true, false>(a, grid, lds, s);
   }
-  return launch_fano_v<HARD, 0, false, RXL>(a, grid, lds, s);
+  return (HARD && rows) ? launch_fano_v<HARD, 0, false, HARD>(a, grid, lds, s)
+                        : launch_fano_v<HARD, 0, false, false>(a, grid, lds, s);
 }
 
 // Persistent lanes: as many waves as the LDS footprint lets the chip hold (256 CUs x 160 KiB), each
-// lane pulls blocks from the queue. The received symbols move into LDS only while the chip still
-// holds four waves per CU (one per SIMD): staging soft K=15 input (864 B per lane) would halve the
-// resident lanes and measured slower (round-1 note in DESIGN.md); hard-decision input always fits.
+// lane pulls blocks from the queue. Received rows move into LDS (ROWS in fano_dev.hpp) only while a
+// wave's footprint stays small (hard input: one byte per node): the search is latency-bound, so the
+// number of resident lanes matters more than the latency of one global load per move -- soft K=15 rows
+// (16 B per node) would cut the chip from 9 to 2 waves per CU and measured 2.8x slower at 4 dB
+// (profiles/r01_fano.txt). CCV_FANO_ROWS=0/1 overrides.
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
-  const size_t node_bytes = (size_t)a.T * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1);
-  const size_t rx_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : (sizeof(float) << a.n));
-  bool rxl = node_bytes + rx_bytes <= 40 * 1024;
-  if (const char* env = std::getenv("CCV_FANO_RXL")) rxl = env[0] == '1' && node_bytes + rx_bytes <= 80 * 1024;
-  const size_t lds = node_bytes + (rxl ? rx_bytes : 0);
+  const size_t node_bytes = ((size_t)(a.T + 1) * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1) + 15) & ~(size_t)15;
+  const size_t row_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : 16);
+  const bool rows_ok = (hard || (a.n == 2 && a.K <= 32)) && node_bytes + row_bytes <= 80 * 1024;
+  bool rows = rows_ok && node_bytes + row_bytes <= 24 * 1024;
+  if (const char* env = std::getenv("CCV_FANO_ROWS")) rows = rows_ok && env[0] == '1';
+  const size_t lds = node_bytes + (rows ? row_bytes : 0);
   const int per_cu = (int)((160 * 1024) / lds) < 32 ? (int)((160 * 1024) / lds) : 32;
   const int resident = 256 * (per_cu > 0 ? per_cu : 1);
   const int waves_needed = (a.nblocks + kFanoThreads - 1) / kFanoThreads;
   const int grid = waves_needed < resident ? waves_needed : resident;
-  if (hard) return rxl ? launch_fano_h<true, true>(a, grid, lds, s) : launch_fano_h<true, false>(a, grid, lds, s);
-  return rxl ? launch_fano_h<false, true>(a, grid, lds, s) : launch_fano_h<false, false>(a, grid, lds, s);
+  return hard ? launch_fano_h<true>(a, rows, grid, lds, s) : launch_fano_h<false>(a, rows, grid, lds, s);
 }
 
 }  // namespace ccv
