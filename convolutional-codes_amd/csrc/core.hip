@@ -3,6 +3,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -450,6 +451,7 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   a.info = d_info;
   a.err = d_info ? d_errors : nullptr;
   a.iterations = d_iterations;
+  if (const char* env = std::getenv("CCV_FANO_COUNT_MOVES")) a.count_moves = env[0] == '1';
   HIP_TRY(ccv::launch_fano(a, p->d.channel == CCV_HARD, stream));
   return 0;
 }

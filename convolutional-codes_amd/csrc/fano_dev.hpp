@@ -43,6 +43,8 @@ struct FanoArgs {
   const uint8_t* info;       // optional: count bit errors
   unsigned long long* err;
   uint32_t* iterations;      // optional [nb]: search iterations used (timeout = 10000 * T)
+  int count_moves;           // diagnostics (CCV_FANO_COUNT_MOVES=1): `iterations` gets the number of
+                             // moves (forward, back, threshold relaxations) instead
 };
 
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
@@ -126,8 +128,8 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       t1 = d1 * a.bm1 + (n - d1) * a.bm0;
     } else {
       float r0, r1;
-      if constexpr (ROWS) {
-        const float4 v = row.v;
+      if constexpr (ROWS || NP == 2) {   // rate 1/2: the node's whole row is one 16-byte load
+        const float4 v = ROWS ? row.v : reinterpret_cast<const float4*>(rx)[d];
         r0 = (e0 & 2u) ? ((e0 & 1u) ? v.w : v.z) : ((e0 & 1u) ? v.y : v.x);
         r1 = (e1 & 2u) ? ((e1 & 1u) ? v.w : v.z) : ((e1 & 1u) ? v.y : v.x);
       } else {
@@ -150,6 +152,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   MT mcur = 0, thr = 0, tm0 = 0, tm1 = 0;
   uint32_t sel = 0, dec = 0, timeout = 0;
   bool inback = false, moved = false;
+  uint32_t moves = 0;
   FanoRow<HARD, NP> row0{};   // received row of node cur
   // start a search (:108-124 reset, then the root's branch metrics)
   auto start = [&]() {
@@ -177,6 +180,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     flags[lane] = (uint8_t)(dec << 1);
     timeout = budget;
     inback = false;
+    moves = 0;
   };
   // output_data (:315-325): the decoded input of every node, MSB-first; nodes past the frontier
   // were never visited and still hold the reset value 0
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       // the metric of the newest received node (:195, :269): the last node when done
       if (a.path_metric) a.path_metric[b] = metric[(done ? T - 1 : frontier) * kFanoThreads + lane];
     }
-    if (a.iterations) a.iterations[b] = budget - timeout;
+    if (a.iterations) a.iterations[b] = a.count_moves ? moves : budget - timeout;
   };
 
   if (b >= (unsigned int)a.nblocks) return;
@@ -251,6 +255,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     inback = bstep && !untried;
     moved = bstep || was_moved;
     const bool need = fwd || (relax && was_moved) || (bstep && untried);
+    moves += (fwd || relax || bstep) ? 1u : 0u;
     frontier = fwd && ncur > frontier ? ncur : frontier;
     cur = ncur;
     if (__builtin_expect(expired || (fwd && ncur == T), 0)) {

@@ -1,6 +1,7 @@
 // stack.hip -- launches of the sequential decoders: the wave-per-block stack decoder (stack_dev.hpp)
 // and the lane-per-block Fano decoder (fano_dev.hpp). Built with -ffp-contract=off: the branch
 // metrics' float product and double sum must not fuse.
+#include <cstdio>
 #include <cstdlib>
 
 #include "fano_dev.hpp"
@@ -40,33 +41,45 @@ hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
   return launch_pw<false, 10>(a, lds, s);
 }
 
+// Persistent lanes: exactly as many waves as the chip holds at once (occupancy query: a wave that
+// is not resident from the start would only begin after a resident one has finished its whole
+// share, doubling the launch), each lane pulling blocks from the queue.
 template <bool HARD, int NP, bool W32, bool ROWS>
-static hipError_t launch_fano_v(const FanoArgs& a, int grid, size_t lds, hipStream_t s) {
+static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
   const void* fn = reinterpret_cast<const void*>(&fano_decode<HARD, NP, W32, ROWS>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
+  int dev = 0, cus = 0, per_cu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kFanoThreads, lds);
+  if (e != hipSuccess) return e;
+  const int resident = (cus > 0 ? cus : 1) * (per_cu > 0 ? per_cu : 1);
+  const int waves_needed = (a.nblocks + kFanoThreads - 1) / kFanoThreads;
+  const int grid = waves_needed < resident ? waves_needed : resident;
+  if (std::getenv("CCV_FANO_DEBUG"))
+    std::fprintf(stderr, "fano: lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n", lds, per_cu, cus, grid);
   hipLaunchKernelGGL((fano_decode<HARD, NP, W32, ROWS>), dim3(grid), dim3(kFanoThreads), lds, s, a);
   return hipGetLastError();
 }
 
 template <bool HARD>
-static hipError_t launch_fano_h(const FanoArgs& a, bool rows, int grid, size_t lds, hipStream_t s) {
+static hipError_t launch_fano_h(const FanoArgs& a, bool rows, size_t lds, hipStream_t s) {
   if (a.K <= 32) {
     if (a.n == 2)
-      return rows ? launch_fano_v<HARD, 2, true, true>(a, grid, lds, s)
-                  : launch_fano_v<HARD, 2, true, false>(a, grid, lds, s);
+      return rows ? launch_fano_v<HARD, 2, true, true>(a, lds, s)
+                  : launch_fano_v<HARD, 2, true, false>(a, lds, s);
     if (a.n == 3)
-      return (HARD && rows) ? launch_fano_v<HARD, 3, true, HARD>(a, grid, lds, s)
-                            : launch_fano_v<HARD, 3, true, false>(a, grid, lds, s);
+      return (HARD && rows) ? launch_fano_v<HARD, 3, true, HARD>(a, lds, s)
+                            : launch_fano_v<HARD, 3, true, false>(a, lds, s);
   }
-  return (HARD && rows) ? launch_fano_v<HARD, 0, false, HARD>(a, grid, lds, s)
-                        : launch_fano_v<HARD, 0, false, false>(a, grid, lds, s);
+  return (HARD && rows) ? launch_fano_v<HARD, 0, false, HARD>(a, lds, s)
+                        : launch_fano_v<HARD, 0, false, false>(a, lds, s);
 }
 
-// Persistent lanes: as many waves as the LDS footprint lets the chip hold (256 CUs x 160 KiB), each
-// lane pulls blocks from the queue. Received rows move into LDS (ROWS in fano_dev.hpp) only while a
+// Received rows move into LDS (ROWS in fano_dev.hpp) only while a
 // wave's footprint stays small (hard input: one byte per node): the search is latency-bound, so the
 // number of resident lanes matters more than the latency of one global load per move -- soft K=15 rows
 // (16 B per node) would cut the chip from 9 to 2 waves per CU and measured 2.8x slower at 4 dB
@@ -78,11 +91,7 @@ hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
   bool rows = rows_ok && node_bytes + row_bytes <= 24 * 1024;
   if (const char* env = std::getenv("CCV_FANO_ROWS")) rows = rows_ok && env[0] == '1';
   const size_t lds = node_bytes + (rows ? row_bytes : 0);
-  const int per_cu = (int)((160 * 1024) / lds) < 32 ? (int)((160 * 1024) / lds) : 32;
-  const int resident = 256 * (per_cu > 0 ? per_cu : 1);
-  const int waves_needed = (a.nblocks + kFanoThreads - 1) / kFanoThreads;
-  const int grid = waves_needed < resident ? waves_needed : resident;
-  return hard ? launch_fano_h<true>(a, rows, grid, lds, s) : launch_fano_h<false>(a, rows, grid, lds, s);
+  return hard ? launch_fano_h<true>(a, rows, lds, s) : launch_fano_h<false>(a, rows, lds, s);
 }
 
 }  // namespace ccv
