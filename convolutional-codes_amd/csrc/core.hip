@@ -452,7 +452,21 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   a.err = d_info ? d_errors : nullptr;
   a.iterations = d_iterations;
   if (const char* env = std::getenv("CCV_FANO_COUNT_MOVES")) a.count_moves = env[0] == '1';
+  const bool debug = std::getenv("CCV_FANO_DEBUG") != nullptr;
+  if (debug) {   // diagnostics: synchronous, prints lane utilisation
+    if (p->counter.grow(32, stream)) return -1;
+    a.next_block = static_cast<unsigned int*>(p->counter.ptr);
+    a.stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(p->counter.ptr) + 16);
+    HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, 32, stream));
+  }
   HIP_TRY(ccv::launch_fano(a, p->d.channel == CCV_HARD, stream));
+  if (debug) {
+    unsigned long long st[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(st, a.stats, sizeof st, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    std::fprintf(stderr, "fano: %zu blocks, wave passes %llu, busy lane passes %llu, lane utilisation %.3f\n",
+                 nblocks, st[0], st[1], st[0] ? (double)st[1] / (64.0 * (double)st[0]) : 0.0);
+  }
   return 0;
 }
 

@@ -45,17 +45,21 @@ struct FanoArgs {
   uint32_t* iterations;      // optional [nb]: search iterations used (timeout = 10000 * T)
   int count_moves;           // diagnostics (CCV_FANO_COUNT_MOVES=1): `iterations` gets the number of
                              // moves (forward, back, threshold relaxations) instead
+  unsigned long long* stats; // diagnostics (CCV_FANO_DEBUG): [0] sum over waves of loop passes,
+                             // [1] sum over lanes of passes in which the lane had a search to advance
 };
 
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
 constexpr int kFanoThreads = 64;
 
-// Received-symbol storage per lane:
-//   ROWS (hard input, or soft rate-1/2): the block's symbols are copied into LDS when a lane takes
-//   the block, one row per node ([T][64] bytes / float4s), and each search step prefetches the rows
-//   of the two nodes it can move to (cur - 1, cur + 1) while the lane keeps its own node's row in
-//   registers: no memory latency after the move is decided.
-//   otherwise: branch metrics read r[e] straight from the block in global memory.
+// Received-symbol access per lane (RM):
+//   kRowsDirect: the branch metrics of the node a move lands on read r[e] from global memory after
+//     the move is decided (any code).
+//   kRowsGlobal: each pass first issues the loads of the two rows a move can land on (cur - 1,
+//     cur + 1) and the lane keeps its own node's row in registers, so the load latency overlaps the
+//     pass instead of following it (hard input or rate 1/2: a row is a byte or a float4).
+//   kRowsLds: as kRowsGlobal, the block's rows copied into LDS when the lane takes the block.
+constexpr int kRowsDirect = 0, kRowsGlobal = 2, kRowsLds = 1;
 template <bool HARD, int NP>
 struct FanoRow;
 template <int NP>
@@ -82,12 +86,13 @@ struct FanoRow<false, NP> {
 // Here every pass of the kernel loop is ONE move -- forward, one step back, or a threshold
 // relaxation -- so all lanes of a wave stay in the same code whatever phase their searches are in,
 // and the branch metrics of the node a lane lands on are computed by one shared piece of code.
-template <bool HARD, int NP, bool W32, bool ROWS>
+template <bool HARD, int NP, bool W32, int RM>
 __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   using MT = typename std::conditional<HARD, int32_t, float>::type;
   using ET = typename std::conditional<HARD, uint8_t, float>::type;
   using ST = typename std::conditional<W32, uint32_t, uint64_t>::type;
-  static_assert(!ROWS || HARD || NP == 2, "rows of received symbols are a byte or a float4");
+  static_assert(RM == kRowsDirect || HARD || NP == 2, "rows of received symbols are a byte or a float4");
+  constexpr bool ROWS = RM != kRowsDirect;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const int T = a.T, K = a.K, n = a.n;
@@ -108,10 +113,16 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
   const uint32_t budget = (uint32_t)kFanoTimeoutPerBit * (uint32_t)T;
 
+  const ET* rx = nullptr;
   auto row_at = [&](int d) {
     FanoRow<HARD, NP> r;
-    if constexpr (HARD) r.v = rows[d * kFanoThreads + lane];
-    else r.v = reinterpret_cast<const float4*>(rows)[d * kFanoThreads + lane];
+    if constexpr (RM == kRowsLds) {
+      if constexpr (HARD) r.v = rows[d * kFanoThreads + lane];
+      else r.v = reinterpret_cast<const float4*>(rows)[d * kFanoThreads + lane];
+    } else {
+      if constexpr (HARD) r.v = rx[d];
+      else r.v = reinterpret_cast<const float4*>(rx)[d];
+    }
     return r;
   };
   // get_transition_metric + sort (:160-181, :213-236) for the node at depth d with state st, whose
@@ -146,7 +157,6 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
 
   // per-lane search state
   unsigned int b = atomicAdd(a.next_block, 1u);
-  const ET* rx = nullptr;
   int cur = 0, frontier = 0;
   ST st = 0;
   MT mcur = 0, thr = 0, tm0 = 0, tm1 = 0;
@@ -157,7 +167,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   // start a search (:108-124 reset, then the root's branch metrics)
   auto start = [&]() {
     rx = in + (size_t)b * T * NS;
-    if constexpr (ROWS) {
+    if constexpr (RM == kRowsLds) {
       if constexpr (HARD) {
         for (int d = 0; d < T; ++d) rows[d * kFanoThreads + lane] = rx[d];
       } else {
@@ -165,8 +175,8 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
         float4* dst = reinterpret_cast<float4*>(rows);
         for (int d = 0; d < T; ++d) dst[d * kFanoThreads + lane] = src[d];
       }
-      row0 = row_at(0);
     }
+    if constexpr (ROWS) row0 = row_at(0);
     metric[lane] = (MT)0;
     cur = 0;
     frontier = 0;
@@ -208,12 +218,14 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     if (a.iterations) a.iterations[b] = a.count_moves ? moves : budget - timeout;
   };
 
-  if (b >= (unsigned int)a.nblocks) return;
+  uint32_t lane_passes = 0;
+  if (b < (unsigned int)a.nblocks) {
   start();
   // One move per pass, computed without branches (a lone lane's search is latency-bound and every
   // taken branch costs the wave an instruction-fetch bubble); stores that a lane does not need go
   // to the spare node row T.
   for (;;) {
+    ++lane_passes;
     // everything a backward move can read, fetched before the move is decided
     const int cm = cur > 0 ? cur - 1 : 0;
     const MT mprev = metric[cm * kFanoThreads + lane];
@@ -275,6 +287,12 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     dec = fwd ? sw : dec;
     const bool wflag = fwd || flip || (bstep && untried);
     flags[(wflag ? ncur : T) * kFanoThreads + lane] = (uint8_t)((bstep ? 1u : 0u) | (dec << 1));
+  }
+  }
+  if (a.stats) {   // all lanes again (those without a block skipped the loop)
+    const int32_t wave_passes = wave_max((int32_t)lane_passes);
+    if (lane == 0) atomicAdd(&a.stats[0], (unsigned long long)wave_passes);
+    atomicAdd(&a.stats[1], (unsigned long long)lane_passes);
   }
 }
 

@@ -44,9 +44,9 @@ hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
 // Persistent lanes: exactly as many waves as the chip holds at once (occupancy query: a wave that
 // is not resident from the start would only begin after a resident one has finished its whole
 // share, doubling the launch), each lane pulling blocks from the queue.
-template <bool HARD, int NP, bool W32, bool ROWS>
+template <bool HARD, int NP, bool W32, int RM>
 static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
-  const void* fn = reinterpret_cast<const void*>(&fano_decode<HARD, NP, W32, ROWS>);
+  const void* fn = reinterpret_cast<const void*>(&fano_decode<HARD, NP, W32, RM>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -61,37 +61,43 @@ static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
   const int grid = waves_needed < resident ? waves_needed : resident;
   if (std::getenv("CCV_FANO_DEBUG"))
     std::fprintf(stderr, "fano: lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n", lds, per_cu, cus, grid);
-  hipLaunchKernelGGL((fano_decode<HARD, NP, W32, ROWS>), dim3(grid), dim3(kFanoThreads), lds, s, a);
+  hipLaunchKernelGGL((fano_decode<HARD, NP, W32, RM>), dim3(grid), dim3(kFanoThreads), lds, s, a);
   return hipGetLastError();
 }
 
 template <bool HARD>
-static hipError_t launch_fano_h(const FanoArgs& a, bool rows, size_t lds, hipStream_t s) {
-  if (a.K <= 32) {
-    if (a.n == 2)
-      return rows ? launch_fano_v<HARD, 2, true, true>(a, lds, s)
-                  : launch_fano_v<HARD, 2, true, false>(a, lds, s);
-    if (a.n == 3)
-      return (HARD && rows) ? launch_fano_v<HARD, 3, true, HARD>(a, lds, s)
-                            : launch_fano_v<HARD, 3, true, false>(a, lds, s);
+static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream_t s) {
+  if (a.K <= 32 && a.n == 2) {
+    if (rm == kRowsLds) return launch_fano_v<HARD, 2, true, kRowsLds>(a, lds, s);
+    if (rm == kRowsGlobal) return launch_fano_v<HARD, 2, true, kRowsGlobal>(a, lds, s);
+    return launch_fano_v<HARD, 2, true, kRowsDirect>(a, lds, s);
   }
-  return (HARD && rows) ? launch_fano_v<HARD, 0, false, HARD>(a, lds, s)
-                        : launch_fano_v<HARD, 0, false, false>(a, lds, s);
+  if (a.K <= 32 && a.n == 3) {
+    if (HARD && rm == kRowsLds) return launch_fano_v<HARD, 3, true, HARD ? kRowsLds : kRowsDirect>(a, lds, s);
+    if (HARD && rm == kRowsGlobal) return launch_fano_v<HARD, 3, true, HARD ? kRowsGlobal : kRowsDirect>(a, lds, s);
+    return launch_fano_v<HARD, 3, true, kRowsDirect>(a, lds, s);
+  }
+  if (HARD && rm == kRowsLds) return launch_fano_v<HARD, 0, false, HARD ? kRowsLds : kRowsDirect>(a, lds, s);
+  if (HARD && rm == kRowsGlobal) return launch_fano_v<HARD, 0, false, HARD ? kRowsGlobal : kRowsDirect>(a, lds, s);
+  return launch_fano_v<HARD, 0, false, kRowsDirect>(a, lds, s);
 }
 
-// Received rows move into LDS (ROWS in fano_dev.hpp) only while a
-// wave's footprint stays small (hard input: one byte per node): the search is latency-bound, so the
-// number of resident lanes matters more than the latency of one global load per move -- soft K=15 rows
-// (16 B per node) would cut the chip from 9 to 2 waves per CU and measured 2.8x slower at 4 dB
-// (profiles/r01_fano.txt). CCV_FANO_ROWS=0/1 overrides.
+// Received rows (fano_dev.hpp, RM): in LDS for hard input (one byte per node, the footprint stays
+// small); for soft input read after the move (kRowsDirect). Measured at the bench size
+// (profiles/r01_fano.txt): soft K=15 rows in LDS (16 B per node) cut the chip from 9 to 2 waves per
+// CU and run 4x slower; prefetching the two candidate rows from global memory runs ~10 % slower --
+// under load the pass is bound by instruction issue, not by the row load. CCV_FANO_ROWS=0/1/2
+// overrides.
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
   const size_t node_bytes = ((size_t)(a.T + 1) * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1) + 15) & ~(size_t)15;
   const size_t row_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : 16);
-  const bool rows_ok = (hard || (a.n == 2 && a.K <= 32)) && node_bytes + row_bytes <= 80 * 1024;
-  bool rows = rows_ok && node_bytes + row_bytes <= 24 * 1024;
-  if (const char* env = std::getenv("CCV_FANO_ROWS")) rows = rows_ok && env[0] == '1';
-  const size_t lds = node_bytes + (rows ? row_bytes : 0);
-  return hard ? launch_fano_h<true>(a, rows, lds, s) : launch_fano_h<false>(a, rows, lds, s);
+  const bool rowable = hard || (a.n == 2 && a.K <= 32);
+  int rm = hard ? kRowsLds : kRowsDirect;
+  if (const char* env = std::getenv("CCV_FANO_ROWS")) rm = rowable ? env[0] - '0' : kRowsDirect;
+  if (rm == kRowsLds && node_bytes + row_bytes > 80 * 1024) rm = kRowsGlobal;
+  if (rm < 0 || rm > 2) rm = kRowsDirect;
+  const size_t lds = node_bytes + (rm == kRowsLds ? row_bytes : 0);
+  return hard ? launch_fano_h<true>(a, rm, lds, s) : launch_fano_h<false>(a, rm, lds, s);
 }
 
 }  // namespace ccv
