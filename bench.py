@@ -152,6 +152,9 @@ def main():
     ap.add_argument("--layout", choices=("block", "step"), default="block",
                     help="input layout in HBM: block-major [nb][T][4] as the reference decoder consumes "
                          "it, or step-major [T][nb][4] (CCV_FLAG_STEP_MAJOR)")
+    ap.add_argument("--decisions", choices=("register", "hbm"), default="register",
+                    help="register: survivor decisions stay in VGPRs where the kernel allows it (K <= 7, "
+                         "r = 1/2, T <= 48); hbm: force the decision scratch array in HBM (A/B)")
     ap.add_argument("--seed", type=int, default=0xC0DE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline work budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -163,7 +166,7 @@ def main():
     import torch.distributed as dist
 
     from ccviterbi import HARD, SOFT, FanoPlan, Plan, StackPlan, channel as ch, named_code
-    from ccviterbi.decoder import FLAG_STEP_MAJOR
+    from ccviterbi.decoder import FLAG_GLOBAL_DECISIONS, FLAG_STEP_MAJOR
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -203,7 +206,8 @@ def main():
     elif args.decoder == "fano":
         plan = FanoPlan(code, chan)
     else:
-        plan = Plan(code, chan, FLAG_STEP_MAJOR if args.layout == "step" else 0)
+        plan = Plan(code, chan, (FLAG_STEP_MAJOR if args.layout == "step" else 0) |
+                    (FLAG_GLOBAL_DECISIONS if args.decisions == "hbm" else 0))
     plan.reserve(nb)
     stream = torch.cuda.current_stream()
 
@@ -317,6 +321,7 @@ def main():
                 **({"p_ppm": args.p_ppm} if hard else {"ebn0_db": args.ebn0}),
                 "parallelism": f"dp{world} (frames sharded, counters all-reduced once)",
                 "kernel": plan.kernel,
+                "decisions": plan.decisions,
                 "input_layout": ("block-major [nb][T] symbols (reference)" if hard else
                                  "block-major [nb][T][2^n] (reference)" if args.layout == "block"
                                  else "step-major [T][nb][2^n]"),

@@ -18,6 +18,7 @@ from .code import GEN_REF_X86, HARD, SOFT, Code
 KERNEL_REGISTER, KERNEL_GENERIC, KERNEL_MULTILANE, KERNEL_STACK, KERNEL_FANO = 1, 2, 3, 4, 5
 FLAG_GENERIC = 1
 FLAG_STEP_MAJOR = 2
+FLAG_GLOBAL_DECISIONS = 4   # survivor decisions through an HBM scratch array (A/B vs register-resident)
 
 
 class DecoderError(RuntimeError):
@@ -70,6 +71,11 @@ class Plan:
         return {KERNEL_REGISTER: "register", KERNEL_GENERIC: "generic",
                 KERNEL_MULTILANE: "multilane", KERNEL_STACK: "stack",
                 KERNEL_FANO: "fano"}[self.desc.kernel]
+
+    @property
+    def decisions(self):
+        """Where survivor decisions live during a decode: "none", "hbm" or "registers"."""
+        return {0: "none", 1: "hbm", 2: "registers"}[self._lib.ccv_plan_decision_storage(self._h)]
 
     def trellis(self) -> np.ndarray:
         out = np.zeros((self.desc.states, 2), np.uint8)

@@ -390,6 +390,131 @@ void viterbi_soft_reg(RegArgs a) {
   accumulate_errors(a, errors);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-resident decisions (r = 1/2 codes, K <= 7, T <= kRegDecMaxChunks * 8).
+//
+// The decision bits of a whole block (T x 2^(K-1) bits: 368 B at K=7, T=46) stay in VGPRs, so the
+// kernel writes no decision scratch and its traceback reads no memory: HBM traffic is the input
+// stream plus the output bytes (decisions are part of the algorithmic bytes, but
+// they never leave the chip). The price is ~96 more VGPRs, i.e. 2 waves per SIMD instead of 3.
+//
+// The block is cut into 8-step chunks that end at step T: the first chunk is padded in FRONT with
+// `pad = 8*nch - T` neutral steps whose branch metrics are {0 for symbol 0, +inf otherwise}. From the
+// reset metrics (0, +inf, ...) such a step reproduces them exactly (state 0 -> 0 via symbol 0; every
+// other new state sees +inf), provided the input-1 branch out of state 0 has a non-zero expected
+// symbol (checked on the host). Every chunk is then a full straight-line 8-step chunk, and decision
+// word u of chunk c belongs to real step 8c + u - pad: static register indices throughout.
+constexpr int kRegDecMaxChunks = 6;
+
+template <CodeSpec C, int MAXC = kRegDecMaxChunks>
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void viterbi_soft_regdec(RegArgs a) {
+  constexpr int S = 1 << (C.K - 1);
+  constexpr int NS = 1 << C.n;
+  static_assert(NS == 4, "register-resident decisions: 16-byte steps (r = 1/2)");
+  constexpr int PF = 8;                      // steps per chunk
+  constexpr int UPR = PF;                    // 16-byte units per block per chunk (one per step)
+  constexpr int ROWB = UPR * 16;
+  constexpr int GRP = 16 / UPR;
+  using DW = DecWord<S>;
+  const int lane = threadIdx.x;
+  const int block0 = blockIdx.x * kRegThreads;
+  const int b = block0 + lane;
+  const int T = a.T, nb = a.nblocks;
+  const int nch = (T + PF - 1) / PF;         // host guarantees 1 <= nch <= MAXC
+  const int pad = nch * PF - T;
+  float M[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) M[s] = s ? __builtin_inff() : 0.0f;   // viterbi-decoder.c:212-218
+
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kRegThreads * ROWB];
+  const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
+  const long block_bytes = (long)T * 16;
+  // chunk c holds real steps [c*PF - pad, c*PF - pad + PF); units before step 0 are replaced by the
+  // neutral step after the read, so their source is clamped to step 0
+  auto issue_chunk = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < UPR; ++k) {
+      const int unit = k * kRegThreads + lane;
+      const int r = unit / UPR, j = unit % UPR;
+      const int su = j ^ ((r / GRP) % UPR);
+      const int gb = block0 + r < nb ? block0 + r : nb - 1;
+      long off = ((long)c * PF - pad + su) * 16;
+      off = off < 0 ? 0 : off;
+      __builtin_amdgcn_global_load_lds(in + (size_t)gb * block_bytes + off,
+                                       (lds_ptr_t)(lds + k * kRegThreads * 16), 16, 0, 0);
+    }
+  };
+  const int sw = (lane / GRP) % UPR;
+  const unsigned char* row = lds + lane * ROWB;
+
+  DW D[MAXC][PF];
+  // one copy of the chunk code per chunk index (template expansion, not a loop the unroller may
+  // keep rolled): every D[c][u] index is a constant, so the decisions stay in VGPRs
+  auto chunk_at = [&]<int c>() {
+    if (c < nch) {
+      float4 chunk[UPR];
+#pragma unroll
+      for (int x = 0; x < UPR; ++x) chunk[x] = *reinterpret_cast<const float4*>(row + ((x ^ sw) * 16));
+      if (c + 1 < nch) {
+        // the chunk is in registers once these reads return; only then may the DMA overwrite it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue_chunk(c + 1);                    // lands while this chunk is decoded
+      }
+      if constexpr (c == 0) {
+#pragma unroll
+        for (int x = 0; x < UPR; ++x)
+          if (x < pad) chunk[x] = float4{0.0f, __builtin_inff(), __builtin_inff(), __builtin_inff()};
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const float bm[4] = {chunk[u].x, chunk[u].y, chunk[u].z, chunk[u].w};
+        D[c][u] = acs_step<C, false, float>(M, bm);
+        __builtin_amdgcn_sched_barrier(0);   // schedule step by step: interleaving steps only adds VGPRs
+      }
+    }
+  };
+  issue_chunk(0);
+  [&]<int... cs>(std::integer_sequence<int, cs...>) {
+    (chunk_at.template operator()<cs>(), ...);
+  }(std::make_integer_sequence<int, MAXC>{});
+
+  uint32_t errors = 0;
+  if (b < nb) {
+    float best;
+    uint32_t st = (uint32_t)argmin_state<S, float>(M, __builtin_inff(), best);
+    // traceback (reference :71-90) over register decisions; the decoded bits of steps T-1 ... 0
+    // are shifted in from the top, so bit 63 ends up holding step 0 (MSB-first output)
+    uint64_t bits = 0;
+    auto back_chunk = [&]<int c>() {
+      if (c < nch) {
+#pragma unroll
+        for (int u = PF - 1; u >= 0; --u) {
+          if (c > 0 || u >= pad) {
+            const uint32_t d = (uint32_t)(D[c][u] >> st) & 1u;
+            bits = (bits >> 1) | ((uint64_t)(st >> (C.K - 2)) << 63);
+            st = ((st << 1) & (S - 1)) | d;
+          }
+        }
+      }
+    };
+    [&]<int... cs>(std::integer_sequence<int, cs...>) {
+      (back_chunk.template operator()<MAXC - 1 - cs>(), ...);
+    }(std::make_integer_sequence<int, MAXC>{});
+    const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+    uint8_t* o = a.out + (size_t)b * OB;
+    for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
+    if (a.info != nullptr) {   // consumer AWGN-channel/main.c:118-144: errors in the first blen bits
+      const uint8_t* inf = a.info + (size_t)b * IB;
+      uint64_t ref = 0;
+      for (int k = 0; k < IB; ++k) ref |= (uint64_t)inf[k] << (56 - 8 * k);
+      const uint64_t mask = a.blen >= 64 ? ~0ull : ~(~0ull >> a.blen);
+      errors = (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
+    }
+  }
+  accumulate_errors(a, errors);
+}
+
 // Production input path for block-major soft input: LDS-DMA staging where a step is at least 16
 // bytes (n >= 2) -- 8-step (128-byte) chunks for n = 2, 4-step chunks for n = 3 -- per-lane loads
 // otherwise (tools/kbench.hip compares the paths; profiles/r01_kbench_variants.txt).

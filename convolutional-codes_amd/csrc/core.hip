@@ -78,6 +78,7 @@ struct ccv_plan {
   float metric_weight = 0.0f;        // stack, soft: code_param.metric_weight
   int32_t bit_metrics[2] = {0, 0};   // stack, hard: code_param.bit_metrics
   bool step_major = false;           // soft input layout [T][nblocks][2^n] (CCV_FLAG_STEP_MAJOR)
+  bool global_decisions = false;     // CCV_FLAG_GLOBAL_DECISIONS
   int generic_spt = 1, generic_threads = 64, generic_chunk = 1;
   size_t generic_lds = 0;
   uint8_t* d_exp = nullptr;          // device copy of exp (generic kernel)
@@ -100,6 +101,14 @@ size_t decision_bytes(const ccv_plan& p, size_t nblocks) {
 }
 
 bool register_path(const ccv_plan& p) { return p.reg_index >= 0 || p.multi_index >= 0; }
+
+// The register-resident-decision kernel (acs_reg.hpp viterbi_soft_regdec), or nullptr.
+ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
+  if (p.reg_index < 0 || p.d.channel != CCV_SOFT || p.step_major || p.global_decisions ||
+      export_decisions || p.d.steps > 8 * ccv::kRegDecMaxChunks)
+    return nullptr;
+  return ccv::soft_regdec_launchers()[p.reg_index];
+}
 
 int find_reg_kernel(const ccv_plan& p) {
   using namespace ccv;
@@ -201,6 +210,7 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
     return fail("no HIP device: %s", hipGetErrorString(e));
   }
   p->step_major = (flags & CCV_FLAG_STEP_MAJOR) != 0;
+  p->global_decisions = (flags & CCV_FLAG_GLOBAL_DECISIONS) != 0;
   if (p->step_major && channel != CCV_SOFT) {
     delete p;
     return fail("step-major input is a soft-decision layout");
@@ -277,9 +287,15 @@ int ccv_plan_trellis(const ccv_plan* p, uint8_t* exp) {
   return 0;
 }
 
+int ccv_plan_decision_storage(const ccv_plan* p) {
+  if (!p) return fail("null plan");
+  if (p->stack || p->fano) return CCV_DECISIONS_NONE;
+  return regdec_kernel(*p, false) ? CCV_DECISIONS_REGISTERS : CCV_DECISIONS_HBM;
+}
+
 int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {
   if (!p) return fail("null plan");
-  if (!register_path(*p)) return 0;
+  if (!register_path(*p) || regdec_kernel(*p, false)) return 0;   // no decision scratch needed
   return p->dec.grow(decision_bytes(*p, max_blocks), p->stream);
 }
 
@@ -315,14 +331,18 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     a.path_metric = hard ? d_path_metric : nullptr;
     a.info = d_info;
     a.err = d_info ? d_errors : nullptr;
+    const ccv::RegLaunchFn regdec = regdec_kernel(*p, d_decisions != nullptr);
     if (d_decisions) {
       a.dec = d_decisions;
-    } else {
+    } else if (!regdec) {
       if (p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
       a.dec = p->dec.ptr;
     }
     const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
-    if (p->reg_index >= 0) {
+    if (regdec) {
+      // decisions stay in VGPRs: no scratch traffic, traceback from registers
+      HIP_TRY(regdec(a, grid, stream));
+    } else if (p->reg_index >= 0) {
       const ccv::RegLaunchFn* fns =
           hard ? ccv::hard_reg_launchers() : ccv::soft_reg_launchers(p->step_major);
       HIP_TRY(fns[p->reg_index](a, grid, stream));

@@ -46,6 +46,9 @@ inline constexpr size_t kNumMultiCodes = sizeof(kMultiCodes) / sizeof(kMultiCode
 
 using RegLaunchFn = hipError_t (*)(const RegArgs&, int grid, hipStream_t stream);
 const RegLaunchFn* soft_reg_launchers(bool step_major);   // [kNumRegCodes], reg_soft.hip
+// [kNumRegCodes], nullptr where the code has no register-resident-decision kernel; valid for
+// block-major input with T <= 8 * kRegDecMaxChunks and no decision export (reg_soft.hip)
+const RegLaunchFn* soft_regdec_launchers();
 const RegLaunchFn* hard_reg_launchers();   // [kNumRegCodes], reg_hard.hip
 const RegLaunchFn* multi_launchers(bool hard);   // [kNumMultiCodes], reg_multi.hip
 

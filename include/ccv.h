@@ -38,6 +38,8 @@ extern "C" {
 #define CCV_FLAG_GENERIC 1u   /* force the table-driven kernel even if a specialised one exists */
 #define CCV_FLAG_STEP_MAJOR 2u /* soft input is step-major float [T][nblocks][2^n] (coalesced;
                                   register-trellis codes only; ccv_decode_device only)            */
+#define CCV_FLAG_GLOBAL_DECISIONS 4u /* keep survivor decisions in an HBM scratch array even where the
+                                  register-resident-decision kernel applies (A/B measurements)    */
 
 #define CCV_KERNEL_REGISTER 1 /* code-specialised register-trellis kernel                       */
 #define CCV_KERNEL_GENERIC 2  /* table-driven LDS kernel                                        */
@@ -69,6 +71,15 @@ int ccv_plan_describe(const ccv_plan* plan, ccv_plan_desc* desc);
 
 /* Expected-symbol table of the plan's trellis: exp[2*s + i], S*2 bytes. */
 int ccv_plan_trellis(const ccv_plan* plan, uint8_t* exp);
+
+/* Where a ccv_decode_device call without decision export keeps the survivor decisions:
+ * CCV_DECISIONS_NONE (stack / Fano decoders: no trellis), CCV_DECISIONS_HBM (scratch array in device
+ * memory, read back by the traceback) or CCV_DECISIONS_REGISTERS (VGPR-resident for the whole block:
+ * soft r = 1/2 codes with K <= 7 and blen + K - 1 <= 48, block-major input). */
+#define CCV_DECISIONS_NONE 0
+#define CCV_DECISIONS_HBM 1
+#define CCV_DECISIONS_REGISTERS 2
+int ccv_plan_decision_storage(const ccv_plan* plan);
 
 /* Grow the plan's device scratch so decodes of up to max_blocks blocks allocate nothing. */
 int ccv_plan_reserve(ccv_plan* plan, size_t max_blocks);

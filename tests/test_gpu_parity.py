@@ -15,7 +15,7 @@ import oracle_ctypes as O
 from ccviterbi import (CODEBOOK, GEN_REF_X86, GEN_TRUE_PARITY, HARD, K7, K8, K9, SOFT, Code,
                        HardDecoder, Plan, SoftDecoder, channel as ch)
 from ccviterbi import sim
-from ccviterbi.decoder import FLAG_GENERIC
+from ccviterbi.decoder import FLAG_GENERIC, FLAG_GLOBAL_DECISIONS
 from conftest import golden_manifest
 
 pytestmark = pytest.mark.gpu
@@ -43,14 +43,15 @@ def _oracle(c: Code, channel, data):
     return O.viterbi_hard(_ocode(c), data)
 
 
-@pytest.mark.parametrize("flags", [0, FLAG_GENERIC], ids=["register", "generic"])
+@pytest.mark.parametrize("flags", [0, FLAG_GLOBAL_DECISIONS, FLAG_GENERIC],
+                         ids=["register", "register-hbm-decisions", "generic"])
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_golden_fixture(case, flags):
     g = O.load_golden(case["name"])
     c = _code_of(g)
     channel = SOFT if case["channel"] == "awgn" else HARD
     plan = Plan(c, channel, flags)
-    if flags:
+    if flags & FLAG_GENERIC:
         assert plan.kernel == "generic"
     res = plan.decode_host(g["rx"])
     if channel == SOFT:
@@ -72,6 +73,15 @@ def test_register_kernel_selected_for_benchmark_codes():
                 plan = Plan(c.with_(gen_mode=gen), channel)
                 assert plan.kernel == "multilane" and plan.desc.lanes == 1 << (c.K - 7)
         assert Plan(c, SOFT, FLAG_GENERIC).kernel == "generic"
+    # survivor decisions: VGPR-resident for the soft r=1/2 K<=7 benchmark codes at blen 40
+    for c in (K7, K7.with_(gen_mode=GEN_TRUE_PARITY), CODEBOOK[0], CODEBOOK[3]):
+        assert Plan(c, SOFT).decisions == "registers"
+        assert Plan(c, SOFT, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
+        assert Plan(c, HARD).decisions == "hbm"
+    assert Plan(K7.with_(blen=42), SOFT).decisions == "registers"   # T = 48
+    assert Plan(K7.with_(blen=43), SOFT).decisions == "hbm"         # T = 49
+    assert Plan(CODEBOOK[5], SOFT).decisions == "hbm"               # r = 1/3
+    assert Plan(K9, SOFT).decisions == "hbm"
     # a K=9 code without an ahead-of-time kernel falls back to the table-driven kernel
     assert Plan(Code(2, 9, 40, (0xF080000000000000, 0xA980000000000000)), SOFT).kernel == "generic"
 
@@ -160,6 +170,25 @@ def test_seeded_vs_oracle(name, c, channel, flags):
             assert np.array_equal(res, ref)
         else:
             assert np.array_equal(res[0], ref) and np.array_equal(res[1], ref_pm)
+
+
+# Register-resident decisions (viterbi_soft_regdec) cut a block into 8-step chunks ending at step T,
+# padding the first one with 8*ceil(T/8) - T neutral steps: every padding 0..7, both sides of the
+# T <= 48 limit, and T < 8 (one padded chunk only).
+REGDEC_BLENS = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 17, 33, 40, 41, 42, 43, 44]
+
+
+@pytest.mark.parametrize("blen", REGDEC_BLENS)
+@pytest.mark.parametrize("base", [K7, K7.with_(gen_mode=GEN_TRUE_PARITY), CODEBOOK[0], CODEBOOK[3]],
+                         ids=["k7", "k7_true", "code0", "code3"])
+def test_register_decisions_all_paddings(base, blen):
+    c = base.with_(blen=blen)
+    info, rx = ch.awgn_blocks(c, 333, ch.noise_scaling(2.0), 77 + blen)
+    ref = O.viterbi_soft(_ocode(c), rx)
+    for flags in (0, FLAG_GLOBAL_DECISIONS):
+        assert np.array_equal(Plan(c, SOFT, flags).decode_host(rx), ref)
+    tied = np.random.default_rng(blen).integers(-2, 3, size=rx.shape).astype(np.float32)
+    assert np.array_equal(Plan(c, SOFT).decode_host(tied), O.viterbi_soft(_ocode(c), tied))
 
 
 @pytest.mark.parametrize("nb", [1, 2, 63, 64, 65, 127, 1000])
@@ -258,7 +287,7 @@ def test_negative_and_tied_soft_metrics():
     rng = np.random.default_rng(3)
     for c in (K7, CODEBOOK[0], K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
         data = rng.integers(-3, 4, size=(300, c.steps, 4)).astype(np.float32)  # many exact ties
-        for flags in (0, FLAG_GENERIC):
+        for flags in (0, FLAG_GLOBAL_DECISIONS, FLAG_GENERIC):
             assert np.array_equal(Plan(c, SOFT, flags).decode_host(data), O.viterbi_soft(_ocode(c), data))
 
 

@@ -22,6 +22,11 @@ using namespace ccv;
 constexpr CodeSpec kK7Ref = kRegCodes[8];
 constexpr CodeSpec kK7True = kRegCodes[9];
 
+template <CodeSpec C>
+void launch_rd(const RegArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((viterbi_soft_regdec<C>), dim3(grid), dim3(kRegThreads), 0, s, a);
+}
+
 struct Variant {
   const char* name;
   void (*launch)(const RegArgs&, int, hipStream_t);
@@ -41,7 +46,13 @@ int main(int argc, char** argv) {
   std::vector<float> h((size_t)nb * T * NS), hs(h.size());
   std::mt19937 rng(1);
   std::exponential_distribution<float> ex(1.0f);
-  for (auto& x : h) x = ex(rng);
+  if (const char* f = getenv("KB_INPUT")) {   // raw float32 [nb][T][4], e.g. the bench's AWGN frames
+    FILE* fp = fopen(f, "rb");
+    if (!fp || fread(h.data(), 4, h.size(), fp) != h.size()) { fprintf(stderr, "bad KB_INPUT\n"); return 1; }
+    fclose(fp);
+  } else {
+    for (auto& x : h) x = ex(rng);
+  }
   for (int b = 0; b < nb; ++b)
     for (int t = 0; t < T; ++t)
       for (int k = 0; k < NS; ++k) hs[((size_t)t * nb + b) * NS + k] = h[((size_t)b * T + t) * NS + k];
@@ -54,6 +65,10 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_out, (size_t)nb * 6));
   CK(hipMalloc(&d_dec, (size_t)(nb + 63) / 64 * 64 * T * 8));
   CK(hipMalloc(&d_err, 8));
+  uint8_t* d_info = nullptr;
+  CK(hipMalloc(&d_info, (size_t)nb * 5));
+  CK(hipMemset(d_info, 0x5a, (size_t)nb * 5));
+  const bool with_err = getenv("KB_ERR") != nullptr;   // fused error count, as bench.py runs it
   CK(hipMemcpy(d_in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_ins, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
   Variant vs[] = {
@@ -82,6 +97,11 @@ int main(int argc, char** argv) {
       {"true/noload-neither", launch_v<kK7True, kLoadStepMajor, 4, 7>, true},
       {"ref/noload-neither", launch_v<kK7Ref, kLoadStepMajor, 4, 7>, true},
       {"true/noload", launch_v<kK7True, kLoadStepMajor, 4, 4>, true},
+      {"ref/regdec", launch_rd<kK7Ref>, false},
+      {"true/regdec", launch_rd<kK7True>, false},
+      {"ref/dma8-nodecst", launch_v<kK7Ref, kLoadLdsDma, 8, kAblateDecStore>, false},
+      {"ref/dma8-notb", launch_v<kK7Ref, kLoadLdsDma, 8, kAblateTraceback>, false},
+      {"ref/dma8-neither", launch_v<kK7Ref, kLoadLdsDma, 8, 3>, false},
   };
   const int nv = sizeof(vs) / sizeof(vs[0]);
   const char* ring_env = getenv("KB_FRAMES");   // >1: rotate over distinct input copies (> MALL)
@@ -99,13 +119,15 @@ int main(int argc, char** argv) {
       a.in = vs[v].step_major ? (const void*)d_ins : (const void*)d_in;
       a.T = T; a.nblocks = nb; a.blen = 40; a.out = d_out; a.dec = d_dec;
       a.dec_stride = (nb + 63) / 64 * 64;
+      if (with_err) { a.info = d_info; a.err = d_err; }
+      const int burst = getenv("KB_BURST") ? atoi(getenv("KB_BURST")) : 1;   // back-to-back launches
       CK(hipEventRecord(e0, 0));
-      vs[v].launch(a, grid, 0);
+      for (int q = 0; q < burst; ++q) vs[v].launch(a, grid, 0);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float t;
       CK(hipEventElapsedTime(&t, e0, e1));
-      if (r > 0) ms[v].push_back(t);
+      if (r > 0) ms[v].push_back(t / burst);
       if (r == 0) CK(hipMemcpy(outs[v].data(), d_out, outs[v].size(), hipMemcpyDeviceToHost));
     }
   }
