@@ -153,22 +153,23 @@ __device__ __forceinline__ uint32_t multi_dec_pos(uint32_t r, int p) {
 }
 
 // One period (phases 0..n-1) of steps t .. t+n-1, each guarded by t + P < T; slot P of the input
-// ring is consumed by phase P and refilled with step t + P + n.
-template <CodeSpec C, bool SAT, typename MT, int P, class In, class Load, class Metrics>
+// ring is consumed by phase P and refilled with step t + P + n. Each step's decision word goes to
+// sink(std::integral_constant<int, P>, t + P, word): an HBM row or a register.
+template <CodeSpec C, bool SAT, typename MT, int P, class In, class Load, class Metrics, class Sink>
 __device__ __forceinline__ void multi_period(int t, int T, MT (&M)[64], In (&ring)[Multi<C>::n],
-                                             Load& load, Metrics& metrics, uint64_t* dec,
-                                             size_t dstride, bool qb0, bool qb1) {
+                                             Load& load, Metrics& metrics, Sink& sink, bool qb0,
+                                             bool qb1) {
   if constexpr (P < Multi<C>::n) {
     constexpr int n = Multi<C>::n;
     if (t + P < T) {
       MT BM[1 << C.n];
       metrics(ring[P], BM);
-      dec[(size_t)(t + P) * dstride] = multi_step<C, P, SAT, MT>(M, BM, qb0, qb1);
+      sink(std::integral_constant<int, P>{}, t + P, multi_step<C, P, SAT, MT>(M, BM, qb0, qb1));
     }
     const int tn = t + P + n;
     ring[P] = load(tn < T ? tn : T - 1);
     __builtin_amdgcn_sched_barrier(0);
-    multi_period<C, SAT, MT, P + 1>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+    multi_period<C, SAT, MT, P + 1>(t, T, M, ring, load, metrics, sink, qb0, qb1);
   }
 }
 
@@ -260,6 +261,7 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_multi(RegArgs a) {
     else M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
   }
   constexpr int n = X::n;
+  auto sink = [&](auto, int t, uint64_t w) { dec[(size_t)t * dstride] = w; };
   if constexpr (HARD) {
     const uint8_t* p = reinterpret_cast<const uint8_t*>(a.in) + (size_t)bc * T;
     auto load = [&](int t) { return (uint32_t)p[t]; };
@@ -271,9 +273,9 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_multi(RegArgs a) {
 #pragma unroll
     for (int k = 0; k < n; ++k) ring[k] = load(k < T ? k : T - 1);
     // saturation (reference :127-130) only matters while some states are unreachable: period 0
-    multi_period<C, true, MT, 0>(0, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+    multi_period<C, true, MT, 0>(0, T, M, ring, load, metrics, sink, qb0, qb1);
     for (int t = n; t < T; t += n)
-      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, sink, qb0, qb1);
   } else {
     const float* p = reinterpret_cast<const float*>(a.in) + (size_t)bc * T * NS;
     auto load = [&](int t) { return load_soft_step<NS>(p + (size_t)t * NS); };
@@ -285,7 +287,7 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_multi(RegArgs a) {
 #pragma unroll
     for (int k = 0; k < n; ++k) ring[k] = load(k < T ? k : T - 1);
     for (int t = 0; t < T; t += n)
-      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, sink, qb0, qb1);
   }
   MT best;
   const MT sentinel = HARD ? (MT)0xFF00u : (MT)__builtin_inff();
@@ -295,6 +297,123 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_multi(RegArgs a) {
     if (writer && a.path_metric) a.path_metric[blk] = (int32_t)best;
   }
   const uint32_t errors = multi_traceback<C>(a, blk, st, writer);
+  accumulate_errors(a, errors);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Register-resident decisions for the multilane kernel (T <= kMultiRegDecSteps), as
+// viterbi_soft_regdec does for K <= 7: each lane keeps its 64-bit decision word of every step in
+// VGPRs (2 x T registers), so nothing is written to or read back from a decision scratch array. The
+// periods are expanded at compile time (every D[p][P] index is a constant); the traceback walks the
+// group's words with one ds_bpermute per step -- every lane of a group holds the same state, so each
+// lane pre-selects the half of its own word the state's position needs.
+constexpr int kMultiRegDecSteps = 48;
+
+template <CodeSpec C>
+inline constexpr int kMultiRegDecPeriods = (kMultiRegDecSteps + Multi<C>::n - 1) / Multi<C>::n;
+
+template <CodeSpec C, bool HARD, int WAVES = 2>
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
+void viterbi_multi_regdec(RegArgs a) {
+  using X = Multi<C>;
+  using MT = typename std::conditional<HARD, uint32_t, float>::type;
+  constexpr int NS = X::NS;
+  constexpr int n = X::n;
+  constexpr int NP = kMultiRegDecPeriods<C>;
+  const int lane = threadIdx.x;
+  const int q = lane & (X::L - 1);
+  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  const int blk = (blockIdx.x * kRegThreads + lane) / X::L;
+  const int T = a.T, nb = a.nblocks;   // host guarantees T <= NP * n
+  const int bc = blk < nb ? blk : nb - 1;
+  MT M[64];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    if constexpr (HARD) M[r] = (q == 0 && r == 0) ? 0u : 0xFF00u;
+    else M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
+  }
+  uint64_t D[NP][n];
+  auto run = [&](auto& ring, auto& load, auto& metrics) {
+    auto period_at = [&]<int p>() {
+      if (p * n < T) {
+        auto sink = [&](auto Pc, int, uint64_t w) { D[p][decltype(Pc)::value] = w; };
+        // saturation (reference :127-130) only matters while some states are unreachable: period 0
+        multi_period<C, HARD && p == 0, MT, 0>(p * n, T, M, ring, load, metrics, sink, qb0, qb1);
+      }
+    };
+    [&]<int... ps>(std::integer_sequence<int, ps...>) {
+      (period_at.template operator()<ps>(), ...);
+    }(std::make_integer_sequence<int, NP>{});
+  };
+  if constexpr (HARD) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(a.in) + (size_t)bc * T;
+    auto load = [&](int t) { return (uint32_t)p[t]; };
+    auto metrics = [](uint32_t sym, MT (&BM)[NS]) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) BM[k] = __builtin_popcount((uint32_t)k ^ (sym & (uint32_t)(NS - 1)));
+    };
+    uint32_t ring[n];
+#pragma unroll
+    for (int k = 0; k < n; ++k) ring[k] = load(k < T ? k : T - 1);
+    run(ring, load, metrics);
+  } else {
+    const float* p = reinterpret_cast<const float*>(a.in) + (size_t)bc * T * NS;
+    auto load = [&](int t) { return load_soft_step<NS>(p + (size_t)t * NS); };
+    auto metrics = [](const SoftStep<NS>& in, MT (&BM)[NS]) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) BM[k] = in.v[k];
+    };
+    SoftStep<NS> ring[n];
+#pragma unroll
+    for (int k = 0; k < n; ++k) ring[k] = load(k < T ? k : T - 1);
+    run(ring, load, metrics);
+  }
+  MT best;
+  const MT sentinel = HARD ? (MT)0xFF00u : (MT)__builtin_inff();
+  uint32_t st = multi_argmin<C, MT>(M, T % n, q, sentinel, best);
+  const bool writer = q == 0 && blk < nb;
+  if constexpr (HARD) {
+    if (writer && a.path_metric) a.path_metric[blk] = (int32_t)best;
+  }
+  // traceback (reference :71-90) over the group's register decisions, steps T-1 ... 0; decoded bits
+  // are shifted in from the top, so bit 63 ends up holding step 0 (MSB-first output)
+  const int gbase = lane & ~(X::L - 1);
+  uint64_t bits = 0;
+  auto back_step = [&]<int p, int P>() {
+    if (p * n + P < T) {
+      // survivors of step t sit at the phase-(t+1) positions (t mod n = P)
+      const uint32_t phys = rotl_bits(st, P + 1 == n ? 0 : P + 1, n);
+      const uint32_t pos = multi_dec_pos(phys & 63u, P);
+      const uint64_t w = D[p][P];
+      const uint32_t half = pos < 32 ? (uint32_t)w : (uint32_t)(w >> 32);
+      const int src = (gbase + (int)(phys >> 6)) << 2;
+      const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)half);
+      const uint32_t bit = (word >> (pos & 31)) & 1u;
+      bits = (bits >> 1) | ((uint64_t)(st >> (C.K - 2)) << 63);
+      st = ((st << 1) & (X::S - 1)) | bit;
+    }
+  };
+  auto back_period = [&]<int p>() {
+    [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
+      (back_step.template operator()<p, n - 1 - Ps>(), ...);
+    }(std::make_integer_sequence<int, n>{});
+  };
+  [&]<int... ps>(std::integer_sequence<int, ps...>) {
+    (back_period.template operator()<NP - 1 - ps>(), ...);
+  }(std::make_integer_sequence<int, NP>{});
+  uint32_t errors = 0;
+  if (writer) {
+    const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+    uint8_t* o = a.out + (size_t)blk * OB;
+    for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
+    if (a.info != nullptr) {   // consumer AWGN-channel/main.c:118-144: errors in the first blen bits
+      const uint8_t* inf = a.info + (size_t)blk * IB;
+      uint64_t ref = 0;
+      for (int k = 0; k < IB; ++k) ref |= (uint64_t)inf[k] << (56 - 8 * k);
+      const uint64_t mask = a.blen >= 64 ? ~0ull : ~(~0ull >> a.blen);
+      errors = (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
+    }
+  }
   accumulate_errors(a, errors);
 }
 

@@ -337,13 +337,14 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_multi(ChanArgs a)
   Step ring[n];
 #pragma unroll
   for (int k = 0; k < n; ++k) ring[k] = load(k);
+  auto sink = [&](auto, int t, uint64_t w) { dec[(size_t)t * dstride] = w; };
   if constexpr (HARD) {
-    multi_period<C, true, MT, 0>(0, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+    multi_period<C, true, MT, 0>(0, T, M, ring, load, metrics, sink, qb0, qb1);
     for (int t = n; t < T; t += n)
-      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, sink, qb0, qb1);
   } else {
     for (int t = 0; t < T; t += n)
-      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, dec, dstride, qb0, qb1);
+      multi_period<C, false, MT, 0>(t, T, M, ring, load, metrics, sink, qb0, qb1);
   }
   MT best;
   const MT sentinel = HARD ? (MT)0xFF00u : (MT)__builtin_inff();

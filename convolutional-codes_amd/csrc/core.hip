@@ -102,10 +102,16 @@ size_t decision_bytes(const ccv_plan& p, size_t nblocks) {
 
 bool register_path(const ccv_plan& p) { return p.reg_index >= 0 || p.multi_index >= 0; }
 
-// The register-resident-decision kernel (acs_reg.hpp viterbi_soft_regdec), or nullptr.
+// The register-resident-decision kernel (acs_reg.hpp viterbi_soft_regdec, acs_multi.hpp
+// viterbi_multi_regdec), or nullptr.
 ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
-  if (p.reg_index < 0 || p.d.channel != CCV_SOFT || p.step_major || p.global_decisions ||
-      export_decisions || p.d.steps > 8 * ccv::kRegDecMaxChunks)
+  if (p.global_decisions || export_decisions) return nullptr;
+  if (p.multi_index >= 0)
+    return p.d.steps <= ccv::multi_regdec_max_steps(p.d.K)
+               ? ccv::multi_regdec_launchers(p.d.channel == CCV_HARD)[p.multi_index]
+               : nullptr;
+  if (p.reg_index < 0 || p.d.channel != CCV_SOFT || p.step_major ||
+      p.d.steps > 8 * ccv::kRegDecMaxChunks)
     return nullptr;
   return ccv::soft_regdec_launchers()[p.reg_index];
 }

@@ -51,6 +51,10 @@ const RegLaunchFn* soft_reg_launchers(bool step_major);   // [kNumRegCodes], reg
 const RegLaunchFn* soft_regdec_launchers();
 const RegLaunchFn* hard_reg_launchers();   // [kNumRegCodes], reg_hard.hip
 const RegLaunchFn* multi_launchers(bool hard);   // [kNumMultiCodes], reg_multi.hip
+// [kNumMultiCodes], register-resident decisions (acs_multi.hpp viterbi_multi_regdec); valid for
+// T <= multi_regdec_max_steps(K) and no decision export (reg_multi.hip)
+const RegLaunchFn* multi_regdec_launchers(bool hard);
+int multi_regdec_max_steps(int K);
 
 struct ChanArgs;
 using ChanLaunchFn = hipError_t (*)(const ChanArgs&, int grid, hipStream_t stream);

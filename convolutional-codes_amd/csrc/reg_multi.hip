@@ -20,11 +20,36 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make(std::index_sequence<I...>) 
   return {&launch<I, HARD>...};
 }
 
+// two waves per SIMD (a few scratch spills) measured 24.4 Gbit/s at K=9 against 18.4 for the
+// one-wave build that spills to AGPRs only (profiles/r01_k9_regdec.txt)
+template <size_t I, bool HARD>
+hipError_t launch_regdec(const RegArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL((viterbi_multi_regdec<kMultiCodes[I], HARD, 2>), dim3(grid), dim3(kRegThreads), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+template <bool HARD, size_t... I>
+constexpr std::array<RegLaunchFn, sizeof...(I)> make_regdec(std::index_sequence<I...>) {
+  return {&launch_regdec<I, HARD>...};
+}
+
 constexpr auto kSoft = make<false>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kHard = make<true>(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kSoftRegDec = make_regdec<false>(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kHardRegDec = make_regdec<true>(std::make_index_sequence<kNumMultiCodes>{});
 
 }  // namespace
 
 const RegLaunchFn* multi_launchers(bool hard) { return hard ? kHard.data() : kSoft.data(); }
+
+const RegLaunchFn* multi_regdec_launchers(bool hard) {
+  return hard ? kHardRegDec.data() : kSoftRegDec.data();
+}
+
+int multi_regdec_max_steps(int K) {
+  const int n = K - 1;
+  return (kMultiRegDecSteps + n - 1) / n * n;
+}
 
 }  // namespace ccv

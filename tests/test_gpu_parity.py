@@ -81,7 +81,12 @@ def test_register_kernel_selected_for_benchmark_codes():
     assert Plan(K7.with_(blen=42), SOFT).decisions == "registers"   # T = 48
     assert Plan(K7.with_(blen=43), SOFT).decisions == "hbm"         # T = 49
     assert Plan(CODEBOOK[5], SOFT).decisions == "hbm"               # r = 1/3
-    assert Plan(K9, SOFT).decisions == "hbm"
+    # K = 8, 9 (multilane kernel): register-resident up to T = 48 (K9) / 49 (K8), soft and hard
+    for c in (K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
+        assert Plan(c, SOFT).decisions == "registers" and Plan(c, HARD).decisions == "registers"
+        assert Plan(c, SOFT, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
+    assert Plan(K9.with_(blen=41), SOFT).decisions == "hbm"           # T = 49
+    assert Plan(K8.with_(blen=42), SOFT).decisions == "registers"     # T = 49
     # a K=9 code without an ahead-of-time kernel falls back to the table-driven kernel
     assert Plan(Code(2, 9, 40, (0xF080000000000000, 0xA980000000000000)), SOFT).kernel == "generic"
 
@@ -211,13 +216,14 @@ def test_multilane_shapes(K, nb, blen):
     the final argmin and the traceback start from (T = blen + K - 1)."""
     c = (K8 if K == 8 else K9).with_(blen=blen)
     info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), nb * 7 + blen)
-    plan = Plan(c, SOFT)
-    assert plan.kernel == "multilane"
-    assert np.array_equal(plan.decode_host(rx), O.viterbi_soft(_ocode(c), rx))
     info, syms = ch.bsc_blocks(c, nb, 90000, nb * 5 + blen)
-    out, pm = Plan(c, HARD).decode_host(syms)
     ref, ref_pm = O.viterbi_hard(_ocode(c), syms)
-    assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+    for flags in (0, FLAG_GLOBAL_DECISIONS):   # register-resident (T <= 48/49) and HBM decisions
+        plan = Plan(c, SOFT, flags)
+        assert plan.kernel == "multilane"
+        assert np.array_equal(plan.decode_host(rx), O.viterbi_soft(_ocode(c), rx))
+        out, pm = Plan(c, HARD, flags).decode_host(syms)
+        assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
 
 
 def test_multilane_error_count_and_no_decision_export(torch_cuda):
