@@ -73,33 +73,6 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t d, H16 m0, H16 m1) {
   return __builtin_amdgcn_alignbit(d, diff, 31);
 }
 
-// Ordered-integer select: for NON-NEGATIVE fp32 metrics (sign bit clear, +inf allowed) the float
-// order equals the unsigned order of the bit patterns, and the BSC kernel's zero-extended 16-bit
-// metrics are plain unsigned integers. Then the borrow of the full-rate `v_sub_co_u32 a1 - a0` is
-// exactly the reference's strict (m1 < m0) (ties: no borrow, the even predecessor stays), and that
-// one borrow (in VCC) drives both the survivor select (`v_cndmask_b32_e32`) and the decision
-// shift-in (`v_addc_co_u32 d = d + d + borrow`): 3 full-rate issues per state where
-// v_min + v_sub + v_alignbit take 5 (tools/gen_seqbench.py "co_cnd_addc", profiles/r01_seqbench.txt).
-// Soft callers guarantee non-negative inputs per wave (viterbi_soft_regdec checks the sign bits and
-// re-runs the wave on the float path otherwise).
-__device__ __forceinline__ void ord_select(uint32_t& d, uint32_t& n, uint32_t a0, uint32_t a1) {
-  uint32_t diff;
-  asm("v_sub_co_u32_e32 %0, vcc, %3, %4\n\t"
-      "v_cndmask_b32_e32 %1, %4, %3, vcc\n\t"
-      "v_addc_co_u32_e32 %2, vcc, %2, %2, vcc"
-      : "=&v"(diff), "=v"(n), "+v"(d)
-      : "v"(a1), "v"(a0)
-      : "vcc");
-}
-__device__ __forceinline__ void ord_select(uint32_t& d, float& n, float a0, float a1) {
-  uint32_t r;
-  ord_select(d, r, __float_as_uint(a0), __float_as_uint(a1));
-  n = __uint_as_float(r);
-}
-__device__ __forceinline__ void ord_select(uint32_t& d, H16& n, H16 a0, H16 a1) {
-  ord_select(d, n.v, a0.v, a1.v);
-}
-
 template <int NS>
 struct SoftStep {
   float v[NS];
