@@ -155,6 +155,11 @@ def main():
     ap.add_argument("--decisions", choices=("register", "hbm"), default="register",
                     help="register: survivor decisions stay in VGPRs where the kernel allows it (K <= 7, "
                          "r = 1/2, T <= 48); hbm: force the decision scratch array in HBM (A/B)")
+    ap.add_argument("--persistent", choices=("on", "off"), default="on",
+                    help="on: the persistent K <= 7 kernels where they apply (blen 40); off: the "
+                         "one-wave-per-64-blocks kernels (A/B, CCV_FLAG_NO_PERSISTENT)")
+    ap.add_argument("--no-error-count", action="store_true",
+                    help="decode without the fused bit-error count (A/B of its cost; no BER reported)")
     ap.add_argument("--seed", type=int, default=0xC0DE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline work budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -166,7 +171,7 @@ def main():
     import torch.distributed as dist
 
     from ccviterbi import HARD, SOFT, FanoPlan, Plan, StackPlan, channel as ch, named_code
-    from ccviterbi.decoder import FLAG_GLOBAL_DECISIONS, FLAG_STEP_MAJOR
+    from ccviterbi.decoder import FLAG_GLOBAL_DECISIONS, FLAG_NO_PERSISTENT, FLAG_STEP_MAJOR
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -207,12 +212,16 @@ def main():
         plan = FanoPlan(code, chan)
     else:
         plan = Plan(code, chan, (FLAG_STEP_MAJOR if args.layout == "step" else 0) |
-                    (FLAG_GLOBAL_DECISIONS if args.decisions == "hbm" else 0))
+                    (FLAG_GLOBAL_DECISIONS if args.decisions == "hbm" else 0) |
+                    (FLAG_NO_PERSISTENT if args.persistent == "off" else 0))
     plan.reserve(nb)
     stream = torch.cuda.current_stream()
 
     def step():
-        plan.decode_device(d_rx, nb, d_out, d_info=d_info, d_errors=d_err, stream=stream)
+        if args.no_error_count:
+            plan.decode_device(d_rx, nb, d_out, stream=stream)
+        else:
+            plan.decode_device(d_rx, nb, d_out, d_info=d_info, d_errors=d_err, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -282,9 +291,16 @@ def main():
     errors = int(errs.item())
 
     if rank == 0:
+        # SURVEY.md 8(d) prices every decoded bit with its survivor decisions (S/8 bytes per step)
+        # whether or not they reach HBM ("the formula is unchanged, so the fraction stays
+        # comparable"); hbm_bytes_per_bit counts only what must cross HBM for this kernel (decisions
+        # excluded where they stay in VGPRs / LDS), and the PMC traffic what did cross it.
         bpb = algorithmic_bytes_per_bit(code, soft=not hard, decisions=not sequential)
+        on_chip = sequential or getattr(plan, "decisions", "hbm") in ("registers", "lds")
+        hbm_bpb = algorithmic_bytes_per_bit(code, soft=not hard, decisions=not on_chip)
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+        hbm_achieved = hbm_bpb * nb * code.blen / (kernel_ms * 1e-3) / 1e9
         workload_key = f"{args.code}:frames{args.frames}:{args.layout}" + (":bsc" if hard else "")
         traffic = load_pmc_traffic(workload_key)
         cpu = None
@@ -321,6 +337,7 @@ def main():
                 **({"p_ppm": args.p_ppm} if hard else {"ebn0_db": args.ebn0}),
                 "parallelism": f"dp{world} (frames sharded, counters all-reduced once)",
                 "kernel": plan.kernel,
+                "variant": getattr(plan, "variant", plan.kernel),
                 "decisions": plan.decisions,
                 "input_layout": ("block-major [nb][T] symbols (reference)" if hard else
                                  "block-major [nb][T][2^n] (reference)" if args.layout == "block"
@@ -340,6 +357,12 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_bit": round(bpb, 4),
                 "bytes_per_launch": int(bytes_per_launch),
+                "hbm_bytes_per_bit": round(hbm_bpb, 4),
+                "hbm_achieved": round(hbm_achieved, 1),
+                "hbm_frac": round(hbm_achieved / HBM_PEAK_GBS, 4),
+                "traffic_frac": (round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                 if traffic else None),
+                "binding_resource": "VALU issue (compare-select, no MFMA; DESIGN.md 4.6)",
             },
             "cpu_baseline": cpu,
             "fused_channel": fused,

@@ -19,6 +19,7 @@ KERNEL_REGISTER, KERNEL_GENERIC, KERNEL_MULTILANE, KERNEL_STACK, KERNEL_FANO = 1
 FLAG_GENERIC = 1
 FLAG_STEP_MAJOR = 2
 FLAG_GLOBAL_DECISIONS = 4   # survivor decisions through an HBM scratch array (A/B vs register-resident)
+FLAG_NO_PERSISTENT = 8      # skip the persistent K <= 7 kernels (A/B)
 
 
 class DecoderError(RuntimeError):
@@ -74,8 +75,13 @@ class Plan:
 
     @property
     def decisions(self):
-        """Where survivor decisions live during a decode: "none", "hbm" or "registers"."""
-        return {0: "none", 1: "hbm", 2: "registers"}[self._lib.ccv_plan_decision_storage(self._h)]
+        """Where survivor decisions live during a decode: "none", "hbm", "registers" or "lds"."""
+        return {0: "none", 1: "hbm", 2: "registers", 3: "lds"}[self._lib.ccv_plan_decision_storage(self._h)]
+
+    @property
+    def variant(self):
+        """The kernel a decode without decision export runs (ccv_plan_kernel_variant)."""
+        return self._lib.ccv_plan_kernel_variant(self._h).decode()
 
     def trellis(self) -> np.ndarray:
         out = np.zeros((self.desc.states, 2), np.uint8)
@@ -124,9 +130,23 @@ class Plan:
         return out if pm is None else (out, pm)
 
     def close(self):
+        """Release the plan's stream and device scratch (also done when the plan is collected)."""
         if getattr(self, "_h", None):
             self._lib.ccv_plan_destroy(self._h)
             self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class StackPlan(Plan):
@@ -158,12 +178,6 @@ class StackPlan(Plan):
                                                _ptr(d_errors), _ptr(d_status), _stream_handle(stream))
         if rc != 0:
             raise DecoderError(f"ccv_stack_decode_device: {_native.last_error()}")
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 class FanoPlan(Plan):

@@ -1,0 +1,420 @@
+// acs_persist.hpp -- persistent register-trellis Viterbi kernels for K <= 7 (gfx950).
+//
+// Same trellis arithmetic as acs_reg.hpp (one lane = one block, all 2^(K-1) metrics in VGPRs, the ACS
+// of AWGN-channel/viterbi-decoder.c:108-141 / binary-symmetric-channel/viterbi-decoder.c:114-150 in
+// closed form), restructured around three measured costs of viterbi_soft_regdec
+// (profiles/r02_pmc_icache_baseline.txt: its waves issue VALU in only 67 % of their lifetime):
+//
+//  * Growth steps. Every block starts from the reset metrics (0 for state 0, +inf / 0xFF00 elsewhere,
+//    viterbi-decoder.c:212-218 / :222-232), so during the first K-1 steps only the multiples of
+//    2^(K-2-t) are reachable after step t, and each of them has exactly one finite candidate -- the
+//    even predecessor s0 -- because the odd one is still unreachable. The reference keeps s0 on that
+//    compare (m1 = inf is not < m0), so those steps are ONE add per reachable state with decision 0:
+//    126 adds instead of 6 x 64 full ACS at K=7, no decision registers, and the unreachable metrics
+//    are compile-time constants. (Finite inputs; with +-inf or NaN in the input the reference itself
+//    traces back through stale state-matrix entries.)
+//  * No padding, no guards. The kernels are specialised on the block length (the codebook's 40 for
+//    every Viterbi code, common/codebook.c:66-68): chunks are aligned to the block start and every
+//    step, chunk and decision register is static. Other lengths use viterbi_soft_regdec /
+//    viterbi_hard_reg.
+//  * Persistent waves. The grid holds exactly the resident waves; each walks groups of 64 blocks
+//    g, g + grid, ... and the LDS-DMA of the NEXT group's first chunk is issued at the start of the
+//    current group's last chunk, so no wave ever waits for a cold first load and no SIMD idles
+//    between short-lived waves.
+//
+// Survivor decisions of the main steps stay in VGPRs (two 32-bit words per step at K=7), the
+// traceback (reference :71-90 / :75-96) walks them back from the lowest-index minimum, then the
+// growth steps (decision 0), and writes the reference's MSB-first output buffer (tail included).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "acs_reg.hpp"
+
+namespace ccv {
+
+constexpr int kPersistMaxMain = 48;   // main (post-growth) steps with register-resident decisions
+
+// Materialise a decision word where it is produced. Its only use is the traceback, so without this
+// the compiler sinks the whole decision packing there and keeps every raw m1 - m0 alive across the
+// block (hundreds of VGPRs, thousands of spills).
+template <typename DW>
+__device__ __forceinline__ void pin(DW& d) {
+  asm volatile("" : "+v"(d));
+}
+
+// Growth step t (0 <= t < K-1) from the reset metrics: new state ns is reachable iff it is a
+// multiple of 2^(K-2-t); its only finite candidate is M[s0] + bm(s0, i).
+template <CodeSpec C, int t, typename MT>
+__device__ __forceinline__ void growth_step(MT (&M)[1 << (C.K - 1)], const MT (&BM)[1 << C.n],
+                                            MT unreachable) {
+  constexpr int S = 1 << (C.K - 1);
+  constexpr int H = S / 2;
+  constexpr int stride = 1 << (C.K - 2 - t);
+  MT N[S];
+#pragma unroll
+  for (int ns = 0; ns < S; ++ns) {
+    if (ns % stride == 0) {
+      const int i = ns >> (C.K - 2);
+      const int s0 = 2 * (ns & (H - 1));
+      N[ns] = M[s0] + BM[expected_symbol(C, s0, i)];
+    } else {
+      N[ns] = unreachable;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) M[s] = N[s];
+}
+
+// Traceback over register decisions D[0 .. F-1] (main steps, F = blen), then the K-1 growth steps (decision
+// 0 on every path through them). Returns the T decoded bits MSB-aligned: bit 63 = step 0.
+// F_rt == F at run time: the per-8-step guards only cut the code into basic blocks (a fully
+// straight-line kernel makes the register allocator spill thousands of VGPRs; see acs_persist notes).
+template <int K, typename DW, int F>
+__device__ __forceinline__ uint64_t traceback_regs(const DW (&D)[F], uint32_t st, int F_rt) {
+  constexpr int S = 1 << (K - 1);
+  uint64_t bits = 0;
+#pragma unroll
+  for (int m = F - 1; m >= 0; --m) {
+    if (m % 8 == 7 || m == F - 1) {
+      if (m >= F_rt) continue;
+    }
+    const uint32_t d = (uint32_t)(D[m] >> st) & 1u;
+    bits = (bits >> 1) | ((uint64_t)(st >> (K - 2)) << 63);
+    st = ((st << 1) & (S - 1)) | d;
+  }
+#pragma unroll
+  for (int g = 0; g < K - 1; ++g) {
+    bits = (bits >> 1) | ((uint64_t)(st >> (K - 2)) << 63);
+    st = (st << 1) & (S - 1);
+  }
+  return bits;
+}
+
+// Output bytes (MSB-first, reference traceback :88) and the bit errors of the first blen bits
+// against the transmitted info bytes (consumer AWGN-channel/main.c:118-144). Static sizes: runtime
+// byte loops here cost the persistent kernels their register allocation (spills).
+template <int T, int BLEN>
+__device__ __forceinline__ uint32_t emit_block(const RegArgs& a, int b, uint64_t bits, uint64_t ref) {
+  constexpr int OB = (T + 7) >> 3;
+  uint8_t* o = a.out + (size_t)b * OB;
+#pragma unroll
+  for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
+  if (a.info == nullptr) return 0;
+  constexpr uint64_t mask = BLEN >= 64 ? ~0ull : ~(~0ull >> BLEN);
+  return (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
+}
+
+// The block's transmitted info bytes, MSB-aligned (bit 63 = info bit 0), or 0 without error counting.
+template <int BLEN>
+__device__ __forceinline__ uint64_t load_info(const RegArgs& a, int b) {
+  constexpr int IB = (BLEN + 7) >> 3;
+  if (a.info == nullptr) return 0;
+  const uint8_t* p = a.info + (size_t)b * IB;
+  uint64_t ref = 0;
+#pragma unroll
+  for (int k = 0; k < IB; ++k) ref |= (uint64_t)p[k] << (56 - 8 * k);
+  return ref;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Soft decision, r = 1/2 (16-byte steps), block-major input [nb][T][4] staged by LDS-DMA in 8-step
+// (128-byte) chunks per block, XOR-swizzled rows as in viterbi_soft_reg, DOUBLE-buffered two chunks
+// deep: the DMA of chunk c+2 (of this group or the next) is issued as soon as chunk c has been read
+// into registers, so each load has two chunks of ACS to land (persist_bench: waiting on one-deep
+// DMA cost ~25 % of the kernel). The LDS reads are inline asm and every chunk waits with an explicit
+// vmcnt(UPR): the compiler would otherwise wait for ALL outstanding DMAs, including the one still
+// filling the other buffer. Issue order per group (so the UPR most recent VMEM ops at each wait
+// are always the next chunk's DMA, whatever the info / output op counts):
+//   chunk 0: wait | read buf 0 | info loads | DMA(g,2) -> buf 0
+//   chunk c: wait | read buf c%2 | DMA(g,c+2) or DMA(g',c+2-NCH) -> buf c%2 (g' = next group, or a
+//            harmless reload when there is none, so the op count never depends on the group)
+//   end    : argmin, traceback, output stores
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
+  f32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
+enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2 };
+
+template <CodeSpec C, int BLEN, int ABLATE = 0>
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void viterbi_soft_persist(RegArgs a, int ngroups) {
+  constexpr int S = 1 << (C.K - 1);
+  static_assert(C.n == 2, "16-byte trellis steps");
+  constexpr int PF = 8;                       // steps per chunk
+  constexpr int UPR = PF;                     // 16-byte units per block per chunk = DMAs per chunk
+  constexpr int ROWB = UPR * 16;
+  constexpr int GRP = 16 / UPR;
+  constexpr int BUF = kRegThreads * ROWB;     // one chunk of the group: 8 KiB
+  constexpr int G = C.K - 1;                  // growth steps
+  constexpr int T = BLEN + G;                 // trellis steps per block
+  constexpr int NCH = (T + PF - 1) / PF;
+  constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
+  static_assert(BLEN >= 1 && BLEN <= kPersistMaxMain, "decisions of the main steps live in VGPRs");
+  static_assert(NCH >= 4 && NCH % 2 == 0, "buffer = chunk parity across groups");
+  using DW = DecWord<S>;
+  const int lane = threadIdx.x;
+  const int nb = a.nblocks;
+  const int stride_groups = gridDim.x;
+
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
+  const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
+  constexpr uint32_t block_bytes = (uint32_t)T * 16;
+  // DMA k of a chunk: lane l moves 16-byte unit j = l % 8 of block r = 8k + l / 8 of the group, from
+  // swizzled slot su = j ^ (r / 2 % 8) of the block's chunk. The per-lane byte offsets inside a
+  // group are the same for every group and chunk (+ c * 128): computed once, 8 VGPRs; the group
+  // base is wave-uniform (SGPRs) and the chunk offset an immediate, so an issue costs no VALU.
+  uint32_t dma_off[UPR];
+#pragma unroll
+  for (int k = 0; k < UPR; ++k) {
+    const int r = k * (kRegThreads / UPR) + lane / UPR, j = lane % UPR;
+    const int su = j ^ ((r / GRP) % UPR);
+    dma_off[k] = (uint32_t)r * block_bytes + (uint32_t)su * 16;
+  }
+  // Groups holding the batch's last block clamp every unit into the buffer (a lane past the batch
+  // replays block nb-1; a unit past the block end re-reads its last step; neither is ever read).
+  auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
+    if (g * kRegThreads + kRegThreads < nb) {
+      const unsigned char* base = in + (size_t)g * kRegThreads * block_bytes + c * PF * 16;
+#pragma unroll
+      for (int k = 0; k < UPR; ++k)
+        __builtin_amdgcn_global_load_lds(base + dma_off[k], (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16),
+                                         16, 0, 0);
+    } else {
+#pragma unroll
+      for (int k = 0; k < UPR; ++k) {
+        const int r = k * (kRegThreads / UPR) + lane / UPR, j = lane % UPR;
+        const int su = j ^ ((r / GRP) % UPR);
+        const int gb = g * kRegThreads + r < nb ? g * kRegThreads + r : nb - 1;
+        uint32_t off = (uint32_t)(c * PF + su) * 16;
+        off = off < block_bytes ? off : block_bytes - 16;
+        __builtin_amdgcn_global_load_lds(in + (size_t)gb * block_bytes + off,
+                                         (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16), 16, 0, 0);
+      }
+    }
+  };
+  // without error counting the info loads still run (from the input): one instruction stream
+  const uint8_t* info_src = a.info != nullptr ? a.info : reinterpret_cast<const uint8_t*>(a.in);
+  const int info_stride = a.info != nullptr ? IB : 0;
+  const uint32_t rd_base = (uint32_t)(uintptr_t)(lds_ptr_t)lds + (uint32_t)(lane * ROWB) +
+                           (uint32_t)(((lane / GRP) % UPR) * 16);
+
+  uint32_t errors = 0;
+  int g = blockIdx.x;
+  if (!(ABLATE & kPersistNoMem) && g < ngroups) {
+    issue_chunk(g, 0, 0);
+    issue_chunk(g, 1, 1);
+  }
+  for (; g < ngroups; g += stride_groups) {
+    const int b = g * kRegThreads + lane;
+    const bool has_next = g + stride_groups < ngroups;
+    float M[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) M[s] = s ? __builtin_inff() : 0.0f;   // viterbi-decoder.c:212-218
+    DW D[BLEN];
+    uint8_t info[IB];
+
+    // one chunk: wait for its DMA, read its rows, hand the buffer to the DMA two chunks ahead, run
+    // its steps
+    auto chunk_at = [&]<int c>() __attribute__((always_inline)) {
+      f32x4 chunk[UPR];
+      if constexpr ((ABLATE & kPersistNoMem) != 0) {
+        int ln = lane + g;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int x = 0; x < UPR; ++x)
+          chunk[x] = f32x4{(float)((ln + x) & 3), (float)((ln + x + 1) & 3), (float)((ln + 2 * x) & 3),
+                           (float)((ln ^ x) & 3)};
+      } else {
+        wait_vmcnt<UPR>();   // this chunk's DMA has landed; the next chunk's may still be in flight
+        // row x of this lane's block sits at slot x ^ sw: (row base | sw * 16) ^ (x * 16), the array
+        // being 1 KiB aligned
+        [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
+          ((chunk[xs] = lds_read_b128<(c % 2) * BUF>(rd_base ^ (uint32_t)(xs * 16))), ...);
+        }(std::make_integer_sequence<int, UPR>{});
+        // the rows are in registers once these reads return; only then may the DMA overwrite them
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(chunk[0]), "+v"(chunk[1]), "+v"(chunk[2]), "+v"(chunk[3]), "+v"(chunk[4]),
+                       "+v"(chunk[5]), "+v"(chunk[6]), "+v"(chunk[7])
+                     :
+                     : "memory");
+        if constexpr (c == 0) {
+          const int bc = b < nb ? b : nb - 1;
+#pragma unroll
+          for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
+          asm volatile("" ::: "memory");   // keep the info loads before the DMA (issue order above)
+        }
+        if constexpr (c + 2 < NCH) issue_chunk(g, c + 2, c % 2);
+        else issue_chunk(has_next ? g + stride_groups : g, c + 2 - NCH, c % 2);
+      }
+      auto step_at = [&]<int u>() __attribute__((always_inline)) {
+        constexpr int t = c * PF + u;
+        const float bm[4] = {chunk[u].x, chunk[u].y, chunk[u].z, chunk[u].w};
+        if constexpr (t < G) growth_step<C, t, float>(M, bm, __builtin_inff());
+        else if constexpr (t < T) {
+          D[t - G] = acs_step<C, false, float>(M, bm);
+          pin(D[t - G]);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // schedule step by step: interleaving steps only adds VGPRs
+      };
+      [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
+        (step_at.template operator()<us>(), ...);
+      }(std::make_integer_sequence<int, PF>{});
+    };
+    [&]<int... cs>(std::integer_sequence<int, cs...>) __attribute__((always_inline)) {
+      (chunk_at.template operator()<cs>(), ...);
+    }(std::make_integer_sequence<int, NCH>{});
+
+    if constexpr ((ABLATE & kPersistNoTraceback) != 0) {
+      uint64_t x = 0;
+#pragma unroll
+      for (int m = 0; m < BLEN; ++m) x ^= D[m];
+#pragma unroll
+      for (int s = 0; s < S; ++s) x += __float_as_uint(M[s]);
+      if (b < nb) reinterpret_cast<uint64_t*>(a.out)[b] = x;
+    } else {
+      float best;
+      const uint32_t st = (uint32_t)argmin_state<S, float>(M, __builtin_inff(), best);
+      const uint64_t bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
+      uint64_t ref = 0;
+#pragma unroll
+      for (int k = 0; k < IB; ++k) ref |= (uint64_t)info[k] << (56 - 8 * k);
+      // exactly OB byte stores per group (the vmcnt arithmetic above counts them); lanes past the
+      // batch store nothing (exec-masked)
+      if (b < nb) {
+        uint8_t* o = a.out + (size_t)b * OB;
+#pragma unroll
+        for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
+        if (a.info != nullptr) {
+          constexpr uint64_t mask = BLEN >= 64 ? ~0ull : ~(~0ull >> BLEN);
+          errors += (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
+        }
+      }
+    }
+  }
+  // the last group's look-ahead DMAs write LDS: they must land before the workgroup (and its LDS
+  // allocation) ends
+  wait_vmcnt<0>();
+  accumulate_errors(a, errors);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Hard decision (BSC), block-major uint8 [nb][T], whole groups only (the host sends a partial last
+// group to viterbi_hard_reg). A group's 64*T input bytes are contiguous and 4-byte aligned: one
+// LDS-DMA of dwords stages them (double-buffered across groups), each lane reads its step bytes.
+// The ACS runs on 16-bit metrics from the first step: reachable metrics are <= n*T < 0xFF00, so the
+// reference's saturation (binary-symmetric-channel/viterbi-decoder.c:127-130) never binds outside
+// the growth steps, whose unreachable states are the constant 0xFF00.
+constexpr int kHardPersistMaxT = 64;   // staged bytes per block (LDS: 2 x 64 x 64 B)
+
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_read_u8(uint32_t addr) {
+  uint32_t r;
+  asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+template <CodeSpec C, int BLEN>
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void viterbi_hard_persist(RegArgs a, int ngroups) {
+  constexpr int S = 1 << (C.K - 1);
+  constexpr int NS = 1 << C.n;
+  constexpr int PF = 8;
+  constexpr int G = C.K - 1;
+  constexpr int T = BLEN + G;
+  constexpr int NCH = (T + PF - 1) / PF;
+  static_assert(BLEN >= 1 && BLEN <= kPersistMaxMain && T <= kHardPersistMaxT, "register decisions");
+  constexpr uint32_t kMask = NS - 1;   // decoder_input masks to n bits (viterbi-decoder.c:235-237)
+  using DW = DecWord<S>;
+  const int lane = threadIdx.x;
+  const int stride_groups = gridDim.x;
+  constexpr int kBuf = kRegThreads * kHardPersistMaxT;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kBuf];
+  const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
+  constexpr int units = (kRegThreads * T) >> 2;   // dwords per group (64 * T is a multiple of 4)
+  auto issue_group = [&](int g, int buf) __attribute__((always_inline)) {
+    const unsigned char* src = in + (size_t)g * kRegThreads * T;
+#pragma unroll
+    for (int k = 0; k * kRegThreads < units; ++k) {
+      int u = k * kRegThreads + lane;
+      u = u < units ? u : units - 1;   // past the group: clamped (LDS slot never read)
+      __builtin_amdgcn_global_load_lds(src + (size_t)u * 4, (lds_ptr_t)(lds + buf * kBuf + k * kRegThreads * 4),
+                                       4, 0, 0);
+    }
+  };
+
+  uint32_t errors = 0;
+  int g = blockIdx.x;
+  int buf = 0;
+  if (g < ngroups) issue_group(g, 0);
+  for (; g < ngroups; g += stride_groups, buf ^= 1) {
+    const int b = g * kRegThreads + lane;
+    // this group's bytes must have landed before the first read (vmcnt also covers the previous
+    // group's output stores, long retired by now)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (g + stride_groups < ngroups) issue_group(g + stride_groups, buf ^ 1);
+    const uint32_t row_addr = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * kBuf + lane * T);
+    const uint64_t info = load_info<BLEN>(a, b);
+    H16 M[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) M[s].v = s ? 0xFF00u : 0u;   // viterbi-decoder.c:225-228
+    DW D[BLEN];
+    auto chunk_at = [&]<int c>() __attribute__((always_inline)) {
+      if (c * PF >= a.T) return;   // always true: per-chunk basic blocks (see the soft kernel)
+      // inline-asm LDS reads: the compiler would otherwise wait for the NEXT group's DMA (into the
+      // other buffer) before every read, since it cannot tell the buffers apart
+      uint32_t sym[PF];
+      [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
+        ((sym[us] = lds_read_u8<c * PF + us>(row_addr)), ...);
+      }(std::make_integer_sequence<int, PF>{});
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(sym[0]), "+v"(sym[1]), "+v"(sym[2]), "+v"(sym[3]), "+v"(sym[4]), "+v"(sym[5]),
+                     "+v"(sym[6]), "+v"(sym[7]));
+      auto step_at = [&]<int u>() __attribute__((always_inline)) {
+        constexpr int t = c * PF + u;
+        if constexpr (t < T) {
+          H16 BM[NS];
+#pragma unroll
+          for (int k = 0; k < NS; ++k) BM[k].v = (uint32_t)__builtin_popcount((uint32_t)k ^ (sym[u] & kMask));
+          if constexpr (t < G) growth_step<C, t, H16>(M, BM, H16{0xFF00u});
+          else {
+            D[t - G] = acs_step<C, false, H16>(M, BM);
+            pin(D[t - G]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
+        (step_at.template operator()<us>(), ...);
+      }(std::make_integer_sequence<int, PF>{});
+    };
+    [&]<int... cs>(std::integer_sequence<int, cs...>) __attribute__((always_inline)) {
+      (chunk_at.template operator()<cs>(), ...);
+    }(std::make_integer_sequence<int, NCH>{});
+
+    uint32_t Mu[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) Mu[s] = M[s].v & 0xFFFFu;
+    uint32_t best;
+    const uint32_t st = (uint32_t)argmin_state<S, uint32_t>(Mu, 0xFF00u, best);
+    if (a.path_metric) a.path_metric[b] = (int32_t)best;
+    const uint64_t bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
+    errors += emit_block<T, BLEN>(a, b, bits, info);
+  }
+  accumulate_errors(a, errors);
+}
+
+}  // namespace ccv

@@ -79,6 +79,7 @@ struct ccv_plan {
   int32_t bit_metrics[2] = {0, 0};   // stack, hard: code_param.bit_metrics
   bool step_major = false;           // soft input layout [T][nblocks][2^n] (CCV_FLAG_STEP_MAJOR)
   bool global_decisions = false;     // CCV_FLAG_GLOBAL_DECISIONS
+  bool no_persistent = false;        // CCV_FLAG_NO_PERSISTENT
   int generic_spt = 1, generic_threads = 64, generic_chunk = 1;
   size_t generic_lds = 0;
   uint8_t* d_exp = nullptr;          // device copy of exp (generic kernel)
@@ -114,6 +115,15 @@ ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
       p.d.steps > 8 * ccv::kRegDecMaxChunks)
     return nullptr;
   return ccv::soft_regdec_launchers()[p.reg_index];
+}
+
+// The persistent K <= 7 kernel (acs_persist.hpp), or nullptr: codebook block length, block-major
+// input, decisions not exported.
+ccv::RegLaunchFn persist_kernel(const ccv_plan& p, bool export_decisions) {
+  if (p.no_persistent || p.global_decisions || export_decisions || p.reg_index < 0 || p.step_major ||
+      p.d.blen != ccv::kPersistBlen)
+    return nullptr;
+  return ccv::persist_launchers(p.d.channel == CCV_HARD)[p.reg_index];
 }
 
 int find_reg_kernel(const ccv_plan& p) {
@@ -217,6 +227,7 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
   }
   p->step_major = (flags & CCV_FLAG_STEP_MAJOR) != 0;
   p->global_decisions = (flags & CCV_FLAG_GLOBAL_DECISIONS) != 0;
+  p->no_persistent = (flags & CCV_FLAG_NO_PERSISTENT) != 0;
   if (p->step_major && channel != CCV_SOFT) {
     delete p;
     return fail("step-major input is a soft-decision layout");
@@ -296,11 +307,28 @@ int ccv_plan_trellis(const ccv_plan* p, uint8_t* exp) {
 int ccv_plan_decision_storage(const ccv_plan* p) {
   if (!p) return fail("null plan");
   if (p->stack || p->fano) return CCV_DECISIONS_NONE;
-  return regdec_kernel(*p, false) ? CCV_DECISIONS_REGISTERS : CCV_DECISIONS_HBM;
+  if (!register_path(*p)) return CCV_DECISIONS_LDS;   // acs_generic.hpp: a block's decisions in LDS
+  return persist_kernel(*p, false) || regdec_kernel(*p, false) ? CCV_DECISIONS_REGISTERS
+                                                               : CCV_DECISIONS_HBM;
+}
+
+const char* ccv_plan_kernel_variant(const ccv_plan* p) {
+  if (!p) return "";
+  if (p->stack) return "stack";
+  if (p->fano) return "fano";
+  if (!register_path(*p)) return "generic";
+  if (persist_kernel(*p, false)) return "persistent";
+  if (p->multi_index >= 0) return regdec_kernel(*p, false) ? "multilane-regdec" : "multilane";
+  return regdec_kernel(*p, false) ? "register-regdec" : "register";
 }
 
 int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {
   if (!p) return fail("null plan");
+  if (persist_kernel(*p, false)) {
+    // hard: a partial last group of < 64 blocks runs on viterbi_hard_reg with HBM decisions
+    if (p->d.channel != CCV_HARD) return 0;
+    return p->dec.grow(decision_bytes(*p, max_blocks < 64 ? max_blocks : 64), p->stream);
+  }
   if (!register_path(*p) || regdec_kernel(*p, false)) return 0;   // no decision scratch needed
   return p->dec.grow(decision_bytes(*p, max_blocks), p->stream);
 }
@@ -337,6 +365,29 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     a.path_metric = hard ? d_path_metric : nullptr;
     a.info = d_info;
     a.err = d_info ? d_errors : nullptr;
+    if (const ccv::RegLaunchFn persist = persist_kernel(*p, d_decisions != nullptr)) {
+      // decisions in VGPRs, grid = resident waves walking 64-block groups (acs_persist.hpp)
+      const size_t full = nblocks / ccv::kRegThreads, rem = nblocks % ccv::kRegThreads;
+      if (!hard) {
+        HIP_TRY(persist(a, (int)(full + (rem ? 1 : 0)), stream));
+        return 0;
+      }
+      if (full) HIP_TRY(persist(a, (int)full, stream));
+      if (rem) {   // the hard kernel stages whole groups: the partial last one goes to viterbi_hard_reg
+        const size_t done = full * ccv::kRegThreads;
+        ccv::RegArgs r = a;
+        r.in = static_cast<const uint8_t*>(d_in) + done * (size_t)p->d.steps;
+        r.nblocks = (int)rem;
+        r.dec_stride = (int)padded_columns(*p, rem);
+        r.out = d_out + done * (size_t)p->d.out_bytes;
+        r.path_metric = a.path_metric ? a.path_metric + done : nullptr;
+        r.info = d_info ? d_info + done * (size_t)p->d.info_bytes : nullptr;
+        if (p->dec.grow(decision_bytes(*p, rem), stream)) return -1;
+        r.dec = p->dec.ptr;
+        HIP_TRY(ccv::hard_reg_launchers()[p->reg_index](r, 1, stream));
+      }
+      return 0;
+    }
     const ccv::RegLaunchFn regdec = regdec_kernel(*p, d_decisions != nullptr);
     if (d_decisions) {
       a.dec = d_decisions;

@@ -50,6 +50,12 @@ const RegLaunchFn* soft_reg_launchers(bool step_major);   // [kNumRegCodes], reg
 // block-major input with T <= 8 * kRegDecMaxChunks and no decision export (reg_soft.hip)
 const RegLaunchFn* soft_regdec_launchers();
 const RegLaunchFn* hard_reg_launchers();   // [kNumRegCodes], reg_hard.hip
+// [kNumRegCodes] persistent kernels (acs_persist.hpp; the int argument is the number of 64-block
+// groups, the launcher sizes the grid to the resident waves), nullptr where a code has none; valid
+// for blen == kPersistBlen, no decision export; soft: block-major r = 1/2 input, hard: whole groups
+// only (reg_persist.hip)
+constexpr int kPersistBlen = 40;   // common/codebook.c:66-68: every Viterbi code of the codebook
+const RegLaunchFn* persist_launchers(bool hard);
 const RegLaunchFn* multi_launchers(bool hard);   // [kNumMultiCodes], reg_multi.hip
 // [kNumMultiCodes], register-resident decisions (acs_multi.hpp viterbi_multi_regdec); valid for
 // T <= multi_regdec_max_steps(K) and no decision export (reg_multi.hip)

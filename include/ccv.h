@@ -17,7 +17,9 @@
  *   output      uint8_t [nblocks][OB]       MSB-first decoded bits, OB = ceil(T/8), tail bits included
  *   info        uint8_t [nblocks][IB]       transmitted info bits (optional), IB = ceil(blen/8)
  * with T = blen + K - 1.  All functions return 0 on success and -1 on failure (ccv_last_error()).
- * Not thread-safe per plan: use one plan per thread (as the reference decoder handle).
+ * Not thread-safe per plan: use one plan per thread (as the reference decoder handle). A plan owns
+ * device scratch (decision arrays, the Fano work counter) that every decode reuses, so the decodes of
+ * one plan must also be serialised on ONE stream; decodes on several streams need one plan each.
  */
 #ifndef CCV_H
 #define CCV_H
@@ -40,6 +42,7 @@ extern "C" {
                                   register-trellis codes only; ccv_decode_device only)            */
 #define CCV_FLAG_GLOBAL_DECISIONS 4u /* keep survivor decisions in an HBM scratch array even where the
                                   register-resident-decision kernel applies (A/B measurements)    */
+#define CCV_FLAG_NO_PERSISTENT 8u /* do not use the persistent K <= 7 kernels (A/B measurements)    */
 
 #define CCV_KERNEL_REGISTER 1 /* code-specialised register-trellis kernel                       */
 #define CCV_KERNEL_GENERIC 2  /* table-driven LDS kernel                                        */
@@ -74,12 +77,19 @@ int ccv_plan_trellis(const ccv_plan* plan, uint8_t* exp);
 
 /* Where a ccv_decode_device call without decision export keeps the survivor decisions:
  * CCV_DECISIONS_NONE (stack / Fano decoders: no trellis), CCV_DECISIONS_HBM (scratch array in device
- * memory, read back by the traceback) or CCV_DECISIONS_REGISTERS (VGPR-resident for the whole block:
- * soft r = 1/2 codes with K <= 7 and blen + K - 1 <= 48, block-major input). */
+ * memory, read back by the traceback), CCV_DECISIONS_REGISTERS (VGPR-resident for the whole block:
+ * the persistent K <= 7 kernels at blen 40, soft r = 1/2 codes with K <= 7 and blen + K - 1 <= 48,
+ * K = 8, 9 with short blocks) or CCV_DECISIONS_LDS (the generic kernel keeps a block's decisions in
+ * LDS). */
 #define CCV_DECISIONS_NONE 0
 #define CCV_DECISIONS_HBM 1
 #define CCV_DECISIONS_REGISTERS 2
+#define CCV_DECISIONS_LDS 3
 int ccv_plan_decision_storage(const ccv_plan* plan);
+
+/* Name of the kernel a ccv_decode_device call without decision export runs: "persistent",
+ * "register-regdec", "register", "multilane-regdec", "multilane", "generic", "stack" or "fano". */
+const char* ccv_plan_kernel_variant(const ccv_plan* plan);
 
 /* Grow the plan's device scratch so decodes of up to max_blocks blocks allocate nothing. */
 int ccv_plan_reserve(ccv_plan* plan, size_t max_blocks);

@@ -26,7 +26,8 @@ def built_libraries():
     """Build the in-tree libraries once if they are missing (hipcc cross-compiles without a GPU)."""
     import subprocess
     need = [os.path.join(PKG_ROOT, "lib", n) for n in
-            ("libccv_core.so", "libccv_awgn.so", "libccv_bsc.so", "libccv_sim.so")]
+            ("libccv_core.so", "libccv_awgn.so", "libccv_bsc.so", "libccv_sim.so",
+             "libccv_stack_awgn.so", "libccv_stack_bsc.so", "libccv_fano_awgn.so", "libccv_fano_bsc.so")]
     if not all(os.path.exists(p) for p in need):
         subprocess.run(["make", "-C", PKG_ROOT, "-j8"], check=True, capture_output=True)
     if not os.path.exists(os.path.join(REPO, "oracle", "build", "libccoracle.so")):

@@ -15,7 +15,7 @@ import oracle_ctypes as O
 from ccviterbi import (CODEBOOK, GEN_REF_X86, GEN_TRUE_PARITY, HARD, K7, K8, K9, SOFT, Code,
                        HardDecoder, Plan, SoftDecoder, channel as ch)
 from ccviterbi import sim
-from ccviterbi.decoder import FLAG_GENERIC, FLAG_GLOBAL_DECISIONS
+from ccviterbi.decoder import FLAG_GENERIC, FLAG_GLOBAL_DECISIONS, FLAG_NO_PERSISTENT
 from conftest import golden_manifest
 
 pytestmark = pytest.mark.gpu
@@ -73,14 +73,22 @@ def test_register_kernel_selected_for_benchmark_codes():
                 plan = Plan(c.with_(gen_mode=gen), channel)
                 assert plan.kernel == "multilane" and plan.desc.lanes == 1 << (c.K - 7)
         assert Plan(c, SOFT, FLAG_GENERIC).kernel == "generic"
-    # survivor decisions: VGPR-resident for the soft r=1/2 K<=7 benchmark codes at blen 40
+    # survivor decisions: VGPR-resident for the K<=7 benchmark codes at blen 40 (persistent kernels,
+    # soft r = 1/2 and hard), for other soft r = 1/2 blocks up to T = 48 (viterbi_soft_regdec)
     for c in (K7, K7.with_(gen_mode=GEN_TRUE_PARITY), CODEBOOK[0], CODEBOOK[3]):
-        assert Plan(c, SOFT).decisions == "registers"
-        assert Plan(c, SOFT, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
-        assert Plan(c, HARD).decisions == "hbm"
+        for channel in (SOFT, HARD):
+            assert Plan(c, channel).decisions == "registers"
+            assert Plan(c, channel).variant == "persistent"
+            assert Plan(c, channel, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
+        assert Plan(c, SOFT, FLAG_NO_PERSISTENT).variant == "register-regdec"
+        assert Plan(c, HARD, FLAG_NO_PERSISTENT).decisions == "hbm"
+    assert Plan(CODEBOOK[5], HARD).variant == "persistent"           # r = 1/3, hard
     assert Plan(K7.with_(blen=42), SOFT).decisions == "registers"   # T = 48
+    assert Plan(K7.with_(blen=42), SOFT).variant == "register-regdec"
     assert Plan(K7.with_(blen=43), SOFT).decisions == "hbm"         # T = 49
+    assert Plan(K7.with_(blen=42), HARD).decisions == "hbm"
     assert Plan(CODEBOOK[5], SOFT).decisions == "hbm"               # r = 1/3
+    assert Plan(K7, SOFT, FLAG_GENERIC).decisions == "lds"          # acs_generic.hpp
     # K = 8, 9 (multilane kernel): register-resident up to T = 48 (K9) / 49 (K8), soft and hard
     for c in (K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
         assert Plan(c, SOFT).decisions == "registers" and Plan(c, HARD).decisions == "registers"
@@ -194,6 +202,95 @@ def test_register_decisions_all_paddings(base, blen):
         assert np.array_equal(Plan(c, SOFT, flags).decode_host(rx), ref)
     tied = np.random.default_rng(blen).integers(-2, 3, size=rx.shape).astype(np.float32)
     assert np.array_equal(Plan(c, SOFT).decode_host(tied), O.viterbi_soft(_ocode(c), tied))
+
+
+# Persistent K <= 7 kernels (acs_persist.hpp, blen 40): growth steps from the reset metrics, static
+# chunks, waves walking 64-block groups with the next group's input prefetched. Checked against the
+# oracle on ragged batches (partial last group; hard: the partial group on viterbi_hard_reg) and,
+# for batches with many groups per resident wave, against the non-persistent kernels block for block.
+PERSIST_CODES = [("k7", K7), ("k7_true", K7.with_(gen_mode=GEN_TRUE_PARITY)), ("code0", CODEBOOK[0]),
+                 ("code1", CODEBOOK[1]), ("code2_true", CODEBOOK[2].with_(gen_mode=GEN_TRUE_PARITY)),
+                 ("code3", CODEBOOK[3])]
+
+
+@pytest.mark.parametrize("nb", [1, 63, 64, 65, 200, 1999])
+@pytest.mark.parametrize("name,c", PERSIST_CODES, ids=[x[0] for x in PERSIST_CODES])
+def test_persistent_kernels_vs_oracle(name, c, nb):
+    info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(1.5), 300 + nb)
+    plan = Plan(c, SOFT)
+    assert plan.variant == "persistent"
+    assert np.array_equal(plan.decode_host(rx), O.viterbi_soft(_ocode(c), rx))
+    tied = np.random.default_rng(nb).integers(-3, 4, size=rx.shape).astype(np.float32)
+    assert np.array_equal(plan.decode_host(tied), O.viterbi_soft(_ocode(c), tied))
+    info, syms = ch.bsc_blocks(c, nb, 110000, 500 + nb)
+    out, pm = Plan(c, HARD).decode_host(syms)
+    ref, ref_pm = O.viterbi_hard(_ocode(c), syms)
+    assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+
+
+def test_persistent_hard_rate_one_third():
+    c = CODEBOOK[5]
+    for nb in (64, 1000):
+        info, syms = ch.bsc_blocks(c, nb, 90000, nb)
+        plan = Plan(c, HARD)
+        assert plan.variant == "persistent"
+        out, pm = plan.decode_host(syms)
+        ref, ref_pm = O.viterbi_hard(_ocode(c), syms)
+        assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+
+
+@pytest.mark.parametrize("channel", [SOFT, HARD], ids=["soft", "hard"])
+@pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["ref", "true"])
+def test_persistent_many_groups_per_wave(torch_cuda, gen, channel):
+    """8 x 1 M-bit frames + 17 blocks: every resident wave walks several groups, so the cross-group
+    prefetch and the per-group reset are exercised; the output, path metrics and fused error count
+    must equal the non-persistent kernel's block for block (and the oracle's on a subsample)."""
+    torch = torch_cuda
+    c = K7.with_(gen_mode=gen)
+    nb = 8 * FRAME + 17
+    if channel == SOFT:
+        info, data = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 4242)
+    else:
+        info, data = ch.bsc_blocks(c, nb, 60000, 4242)
+    d_in, d_info = _device(torch, data), _device(torch, info)
+    res = []
+    for flags in (0, FLAG_NO_PERSISTENT):
+        plan = Plan(c, channel, flags)
+        d_out = torch.zeros((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+        d_pm = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+        plan.decode_device(d_in, nb, d_out, d_path_metric=d_pm if channel == HARD else None,
+                           d_info=d_info, d_errors=d_err)
+        torch.cuda.synchronize()
+        res.append((d_out.cpu().numpy(), d_pm.cpu().numpy(), int(d_err.item())))
+    (out, pm, err), (out2, pm2, err2) = res
+    assert np.array_equal(out, out2) and np.array_equal(pm, pm2) and err == err2
+    assert err == ch.count_bit_errors(c, info, out)
+    idx = np.arange(0, nb, 211)
+    ref, ref_pm = _oracle(c, channel, data[idx])
+    assert np.array_equal(out[idx], ref)
+    if channel == HARD:
+        assert np.array_equal(pm[idx], ref_pm)
+
+
+def test_dropped_plans_release_device_memory(torch_cuda):
+    """Plan.__del__ destroys the plan: creating and dropping plans with large HBM decision scratch
+    does not leak device memory (nor streams)."""
+    import gc
+    torch = torch_cuda
+    torch.cuda.synchronize()
+    gc.collect()
+    free0, _ = torch.cuda.mem_get_info()
+    for _ in range(12):
+        plan = Plan(K7, SOFT, FLAG_GLOBAL_DECISIONS)
+        plan.reserve(1_600_000)          # ~590 MB of decision scratch each
+        del plan
+    with Plan(K7, HARD, FLAG_GLOBAL_DECISIONS) as plan:
+        plan.reserve(1_600_000)
+    gc.collect()
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    assert free1 >= free0 - (64 << 20), (free0, free1)
 
 
 @pytest.mark.parametrize("nb", [1, 2, 63, 64, 65, 127, 1000])

@@ -1,0 +1,91 @@
+// persist_bench.hip -- timing ablations of the persistent K=7 soft kernel (acs_persist.hpp):
+// full kernel, no input traffic (VALU + traceback only), no traceback, neither; at 2 and 3 waves/SIMD.
+// Build: hipcc -O3 -std=c++20 --offload-arch=gfx950 -fno-slp-vectorize -I../include
+//        -I../convolutional-codes_amd/csrc persist_bench.hip -o persist_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "acs_persist.hpp"
+
+using namespace ccv;
+constexpr CodeSpec kK7Ref{2, 7, {0xF200000000000000ull, 0xB600000000000000ull, 0, 0, 0, 0, 0, 0}, GEN_REF_X86};
+constexpr CodeSpec kK7True{2, 7, {0xF200000000000000ull, 0xB600000000000000ull, 0, 0, 0, 0, 0, 0},
+                           GEN_TRUE_PARITY};
+
+#define CHECK(x)                                                              \
+  do {                                                                        \
+    hipError_t e = (x);                                                       \
+    if (e != hipSuccess) {                                                    \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                  \
+      return 1;                                                               \
+    }                                                                         \
+  } while (0)
+
+template <CodeSpec C, int AB>
+int run(const char* name, RegArgs a, int ngroups, int waves_per_cu, int cus) {
+  auto kern = viterbi_soft_persist<C, 40, AB>;
+  int per_cu = 0;
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
+  const int w = waves_per_cu < per_cu ? waves_per_cu : per_cu;
+  const int grid = w * cus < ngroups ? w * cus : ngroups;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int rep = 0; rep < 12; ++rep) {
+    CHECK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, a, ngroups);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    if (rep >= 2 && ms < best) best = ms;
+  }
+  // sustained: 40 back-to-back launches (as bench.py's timed steps), mean per launch
+  CHECK(hipEventRecord(e0, 0));
+  for (int rep = 0; rep < 40; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, a, ngroups);
+  CHECK(hipEventRecord(e1, 0));
+  CHECK(hipEventSynchronize(e1));
+  float sus = 0;
+  CHECK(hipEventElapsedTime(&sus, e0, e1));
+  sus /= 40;
+  const double bits = (double)ngroups * 64 * 40;
+  printf("%-28s waves/CU %2d (max %2d)  isolated %.4f ms %6.1f Gbit/s  sustained %.4f ms %6.1f Gbit/s\n",
+         name, w, per_cu, best, bits / (best * 1e-3) / 1e9, sus, bits / (sus * 1e-3) / 1e9);
+  return 0;
+}
+
+int main() {
+  const int nb = 1600000, T = 46;
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  std::vector<float> h((size_t)nb * T * 4);
+  uint32_t x = 12345;
+  for (auto& v : h) {
+    x = x * 1664525u + 1013904223u;
+    v = (float)(x >> 8) * (1.0f / 16777216.0f) * 3.0f;
+  }
+  float* d_in;
+  uint8_t* d_out;
+  CHECK(hipMalloc(&d_in, h.size() * 4));
+  CHECK(hipMalloc(&d_out, (size_t)nb * 8));
+  CHECK(hipMemcpy(d_in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  RegArgs a{};
+  a.in = d_in;
+  a.T = T;
+  a.nblocks = nb;
+  a.blen = 40;
+  a.out = d_out;
+  const int ng = nb / 64;
+  for (int w : {8, 12}) {
+    run<kK7Ref, 0>("ref full", a, ng, w, cus);
+    run<kK7Ref, kPersistNoMem>("ref no-mem", a, ng, w, cus);
+    run<kK7Ref, kPersistNoTraceback>("ref no-traceback", a, ng, w, cus);
+    run<kK7Ref, kPersistNoMem | kPersistNoTraceback>("ref no-mem no-traceback", a, ng, w, cus);
+  }
+  run<kK7True, 0>("true full", a, ng, 8, cus);
+  run<kK7True, kPersistNoMem | kPersistNoTraceback>("true no-mem no-traceback", a, ng, 8, cus);
+  return 0;
+}
