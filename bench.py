@@ -158,6 +158,10 @@ def main():
     ap.add_argument("--persistent", choices=("on", "off"), default="on",
                     help="on: the persistent K <= 7 kernels where they apply (blen 40); off: the "
                          "one-wave-per-64-blocks kernels (A/B, CCV_FLAG_NO_PERSISTENT)")
+    ap.add_argument("--clock-warmup", type=float, default=0.3,
+                    help="seconds of untimed decode launches before the W warmup steps: a cold MI355X "
+                         "needs ~40 ms of continuous load to reach its sustained clock (per-launch times "
+                         "fall from 0.51 to 0.33 ms over the first ~80 launches, profiles/r02_clock_ramp.txt)")
     ap.add_argument("--no-error-count", action="store_true",
                     help="decode without the fused bit-error count (A/B of its cost; no BER reported)")
     ap.add_argument("--seed", type=int, default=0xC0DE)
@@ -223,6 +227,12 @@ def main():
         else:
             plan.decode_device(d_rx, nb, d_out, d_info=d_info, d_errors=d_err, stream=stream)
 
+    # bring the GPU to its sustained clock (untimed), then the W warmup steps
+    t_warm = time.perf_counter()
+    while time.perf_counter() - t_warm < args.clock_warmup:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     d_err.zero_()
@@ -347,6 +357,7 @@ def main():
                     "errors": errors, "bits": bits_per_step * args.steps,
                     "ber": errors / (bits_per_step * args.steps)},
             "kernel_ms": round(kernel_ms, 4),
+            "clock_warmup_s": args.clock_warmup,
             "pcie_inclusive_mbit_s": round(nb * code.blen / pcie_s / 1e6, 1) if pcie_s else None,
             "roofline": {
                 "bound": "hbm",

@@ -45,6 +45,50 @@ __device__ __forceinline__ void pin(DW& d) {
   asm volatile("" : "+v"(d));
 }
 
+// ACS step in full-rate instructions only (soft decision): per new state d = m1 - m0 (v_sub),
+// mask = d >> 31 arithmetic (v_ashrrev), survivor = mask ? m1 : m0 (v_bitop3 select), and the
+// decision bit OR-ed into its fixed position of the word (mask & bit, merged by the compiler for
+// states whose masks are the same value). Same decisions and metrics as acs_step: mask = sign of
+// m1 - m0, the survivor is m1 exactly when m1 < m0 (metrics are never -0; see acs_step).
+__device__ __forceinline__ uint32_t sign_mask(float a0, float a1) {
+  float d;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(a1), "v"(a0));
+  uint32_t m;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(m) : "v"(d));
+  return m;
+}
+__device__ __forceinline__ float select_mask(uint32_t m, float a0, float a1) {
+  float n;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(n) : "v"(m), "v"(a1), "v"(a0));   // m ? a1 : a0
+  return n;
+}
+
+template <CodeSpec C>
+__device__ __forceinline__ DecWord<(1 << (C.K - 1))> acs_step_select(float (&M)[1 << (C.K - 1)],
+                                                                     const float (&BM)[1 << C.n]) {
+  constexpr int S = 1 << (C.K - 1);
+  constexpr int H = S / 2;
+  constexpr int W = S > 32 ? 2 : 1;
+  float N[S];
+  uint32_t dw[W] = {};
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float m0 = M[2 * j] + BM[expected_symbol(C, 2 * j, i)];
+      const float m1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, i)];
+      const uint32_t mask = sign_mask(m0, m1);
+      const int ns = j + i * H;
+      N[ns] = select_mask(mask, m0, m1);
+      dw[ns / 32] |= mask & (1u << (ns % 32));
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) M[s] = N[s];
+  if constexpr (S > 32) return ((uint64_t)dw[1] << 32) | dw[0];
+  else return dw[0];
+}
+
 // Growth step t (0 <= t < K-1) from the reset metrics: new state ns is reachable iff it is a
 // multiple of 2^(K-2-t); its only finite candidate is M[s0] + bm(s0, i).
 template <CodeSpec C, int t, typename MT>
@@ -147,7 +191,7 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 }
 
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
-enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2 };
+enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -265,7 +309,8 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
         const float bm[4] = {chunk[u].x, chunk[u].y, chunk[u].z, chunk[u].w};
         if constexpr (t < G) growth_step<C, t, float>(M, bm, __builtin_inff());
         else if constexpr (t < T) {
-          D[t - G] = acs_step<C, false, float>(M, bm);
+          if constexpr ((ABLATE & kPersistSelectAcs) != 0) D[t - G] = acs_step_select<C>(M, bm);
+          else D[t - G] = acs_step<C, false, float>(M, bm);
           pin(D[t - G]);
         }
         __builtin_amdgcn_sched_barrier(0);   // schedule step by step: interleaving steps only adds VGPRs

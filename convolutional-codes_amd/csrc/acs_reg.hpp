@@ -73,6 +73,59 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t d, H16 m0, H16 m1) {
   return __builtin_amdgcn_alignbit(d, diff, 31);
 }
 
+// Insert the decision (m1 < m0) at bit `holes` of (d << (holes + 1)), leaving `holes` don't-care
+// bits below it for positions that are filled by copy_collapsed (v_alignbit takes the top
+// holes + 1 bits of m1 - m0: the sign, then garbage).
+template <int HOLES>
+__device__ __forceinline__ uint32_t shift_in_n(uint32_t d, float m0, float m1) {
+  if constexpr (HOLES == 0) return shift_in(d, m0, m1);
+  else return __builtin_amdgcn_alignbit(d, __float_as_uint(m1 - m0), 31 - HOLES);
+}
+template <int HOLES>
+__device__ __forceinline__ uint32_t shift_in_n(uint32_t d, uint32_t m0, uint32_t m1) {
+  if constexpr (HOLES == 0) return shift_in(d, m0, m1);
+  else return __builtin_amdgcn_alignbit(d, m1 - m0, 31 - HOLES);
+}
+template <int HOLES>
+__device__ __forceinline__ uint32_t shift_in_n(uint32_t d, H16 m0, H16 m1) {
+  uint32_t diff;
+  asm("v_sub_u32_e32 %0, %1, %2" : "=v"(diff) : "v"(m1.v), "v"(m0.v));
+  return __builtin_amdgcn_alignbit(d, diff, 31 - HOLES);
+}
+
+// Butterfly j (old states 2j, 2j+1) is "collapsed" when both old states emit the same symbol for
+// input 0 and input 1 (the x86-idiom codes: 16 of the 32 butterflies of K=7 (171,133)). Then new
+// states j and j + S/2 have bit-identical candidates, hence the same metric (the compiler keeps
+// one) and the same decision: the upper word takes those bits from the lower word with ONE
+// v_bitop3 select instead of one v_alignbit each.
+template <CodeSpec C>
+constexpr bool collapsed_butterfly(int j) {
+  return expected_symbol(C, 2 * j, 0) == expected_symbol(C, 2 * j, 1) &&
+         expected_symbol(C, 2 * j + 1, 0) == expected_symbol(C, 2 * j + 1, 1);
+}
+template <CodeSpec C>
+constexpr uint32_t collapsed_mask() {
+  uint32_t m = 0;
+  for (int j = 0; j < (1 << (C.K - 2)); ++j)
+    if (collapsed_butterfly<C>(j)) m |= 1u << j;
+  return m;
+}
+// consecutive collapsed butterflies directly below j (filled later, skipped by j's insert)
+template <CodeSpec C>
+constexpr int collapsed_below(int j) {
+  int h = 0;
+  for (int k = j - 1; k >= 0 && collapsed_butterfly<C>(k); --k) ++h;
+  return h;
+}
+
+// v_bitop3_b32 truth table index = (src0 << 2) | (src1 << 1) | src2 (checked on the device:
+// tools/acs_unit.hip), so src0 ? src1 : src2 is 0xCA.
+__device__ __forceinline__ uint32_t select_bits(uint32_t mask, uint32_t if_set, uint32_t if_clear) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "s"(mask), "v"(if_set), "v"(if_clear));
+  return r;
+}
+
 template <int NS>
 struct SoftStep {
   float v[NS];
@@ -112,21 +165,40 @@ __device__ __forceinline__ DecWord<(1 << (C.K - 1))> acs_step(MT (&M)[1 << (C.K 
   constexpr int H = S / 2;
   MT N[S];
   uint32_t dlo = 0, dhi = 0;
+  if constexpr (collapsed_mask<C>() == 0) {
 #pragma unroll
-  for (int j = H - 1; j >= 0; --j) {
-    MT a0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 0)];
-    MT a1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 0)];
-    MT b0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 1)];
-    MT b1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 1)];
-    if constexpr (SAT) {  // binary-symmetric-channel/viterbi-decoder.c:127-130
-      a0 = vmin(a0, (MT)0xFF00); a1 = vmin(a1, (MT)0xFF00);
-      b0 = vmin(b0, (MT)0xFF00); b1 = vmin(b1, (MT)0xFF00);
+    for (int j = H - 1; j >= 0; --j) {
+      MT a0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 0)];
+      MT a1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 0)];
+      MT b0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 1)];
+      MT b1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 1)];
+      if constexpr (SAT) {  // binary-symmetric-channel/viterbi-decoder.c:127-130
+        a0 = vmin(a0, (MT)0xFF00); a1 = vmin(a1, (MT)0xFF00);
+        b0 = vmin(b0, (MT)0xFF00); b1 = vmin(b1, (MT)0xFF00);
+      }
+      N[j] = vmin(a0, a1);
+      dlo = shift_in(dlo, a0, a1);
+      N[j + H] = vmin(b0, b1);
+      dhi = shift_in(dhi, b0, b1);
     }
-    N[j] = vmin(a0, a1);
-    dlo = shift_in(dlo, a0, a1);
-    N[j + H] = vmin(b0, b1);
-    dhi = shift_in(dhi, b0, b1);
-  }
+  } else [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
+    ([&]() __attribute__((always_inline)) {
+      constexpr int j = H - 1 - js;   // descending: state j ends up in bit j
+      MT a0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 0)];
+      MT a1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 0)];
+      MT b0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 1)];
+      MT b1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 1)];
+      if constexpr (SAT) {  // binary-symmetric-channel/viterbi-decoder.c:127-130
+        a0 = vmin(a0, (MT)0xFF00); a1 = vmin(a1, (MT)0xFF00);
+        b0 = vmin(b0, (MT)0xFF00); b1 = vmin(b1, (MT)0xFF00);
+      }
+      N[j] = vmin(a0, a1);
+      dlo = shift_in(dlo, a0, a1);
+      N[j + H] = vmin(b0, b1);
+      if constexpr (!collapsed_butterfly<C>(j)) dhi = shift_in_n<collapsed_below<C>(j)>(dhi, b0, b1);
+    }(), ...);
+  }(std::make_integer_sequence<int, H>{});
+  if constexpr (collapsed_mask<C>() != 0) dhi = select_bits(collapsed_mask<C>(), dlo, dhi);
 #pragma unroll
   for (int s = 0; s < S; ++s) M[s] = N[s];
   if constexpr (S > 32) return ((uint64_t)dhi << 32) | dlo;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "acs_persist.hpp"
@@ -57,7 +58,31 @@ int run(const char* name, RegArgs a, int ngroups, int waves_per_cu, int cus) {
   return 0;
 }
 
-int main() {
+// Per-launch times over a long back-to-back run: clock ramp-up vs power throttling.
+template <CodeSpec C>
+int trace(RegArgs a, int ngroups, int waves_per_cu, int cus, int n) {
+  auto kern = viterbi_soft_persist<C, 40, 0>;
+  const int grid = waves_per_cu * cus < ngroups ? waves_per_cu * cus : ngroups;
+  std::vector<hipEvent_t> ev(n + 1);
+  for (auto& evt : ev) CHECK(hipEventCreate(&evt));
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(ev[0], 0));
+  for (int i = 0; i < n; ++i) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, a, ngroups);
+    CHECK(hipEventRecord(ev[i + 1], 0));
+  }
+  CHECK(hipEventSynchronize(ev[n]));
+  printf("trace (ms per launch, mean of 10):");
+  for (int i = 0; i < n; i += 10) {
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 10 < n ? i + 10 : n]));
+    printf(" %.3f", ms / 10);
+  }
+  printf("\n");
+  return 0;
+}
+
+int main(int argc, char** argv) {
   const int nb = 1600000, T = 46;
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -79,12 +104,21 @@ int main() {
   a.blen = 40;
   a.out = d_out;
   const int ng = nb / 64;
+  if (argc > 1) {   // persist_bench trace [launches]
+    const int n = argc > 2 ? atoi(argv[2]) : 300;
+    trace<kK7Ref>(a, ng, 8, cus, n);
+    return 0;
+  }
   for (int w : {8, 12}) {
     run<kK7Ref, 0>("ref full", a, ng, w, cus);
     run<kK7Ref, kPersistNoMem>("ref no-mem", a, ng, w, cus);
     run<kK7Ref, kPersistNoTraceback>("ref no-traceback", a, ng, w, cus);
     run<kK7Ref, kPersistNoMem | kPersistNoTraceback>("ref no-mem no-traceback", a, ng, w, cus);
   }
+  run<kK7Ref, kPersistSelectAcs>("ref select-acs full", a, ng, 8, cus);
+  run<kK7Ref, kPersistSelectAcs | kPersistNoMem | kPersistNoTraceback>("ref select-acs no-mem no-tb", a, ng, 8, cus);
+  run<kK7True, kPersistSelectAcs>("true select-acs full", a, ng, 8, cus);
+  run<kK7True, kPersistSelectAcs | kPersistNoMem | kPersistNoTraceback>("true select-acs no-mem no-tb", a, ng, 8, cus);
   run<kK7True, 0>("true full", a, ng, 8, cus);
   run<kK7True, kPersistNoMem | kPersistNoTraceback>("true no-mem no-traceback", a, ng, 8, cus);
   return 0;
