@@ -165,17 +165,18 @@ __device__ __forceinline__ uint64_t load_info(const RegArgs& a, int b) {
 
 // ------------------------------------------------------------------------------------------------
 // Soft decision, r = 1/2 (16-byte steps), block-major input [nb][T][4] staged by LDS-DMA in 8-step
-// (128-byte) chunks per block, XOR-swizzled rows as in viterbi_soft_reg, DOUBLE-buffered two chunks
-// deep: the DMA of chunk c+2 (of this group or the next) is issued as soon as chunk c has been read
-// into registers, so each load has two chunks of ACS to land (persist_bench: waiting on one-deep
-// DMA cost ~25 % of the kernel). The LDS reads are inline asm and every chunk waits with an explicit
-// vmcnt(UPR): the compiler would otherwise wait for ALL outstanding DMAs, including the one still
-// filling the other buffer. Issue order per group (so the UPR most recent VMEM ops at each wait
-// are always the next chunk's DMA, whatever the info / output op counts):
-//   chunk 0: wait | read buf 0 | info loads | DMA(g,2) -> buf 0
-//   chunk c: wait | read buf c%2 | DMA(g,c+2) or DMA(g',c+2-NCH) -> buf c%2 (g' = next group, or a
-//            harmless reload when there is none, so the op count never depends on the group)
+// (128-byte) chunks per block, XOR-swizzled rows as in viterbi_soft_reg, one chunk in flight: the DMA
+// of chunk c+1 (of this group, or chunk 0 of the next) is issued as soon as chunk c has been read
+// into registers. The LDS reads are inline asm and the waits explicit vmcnt, so the compiler adds
+// none of its own. Issue order per group:
+//   chunk 0: wait | read | info loads | DMA(g,1)
+//   chunk c: wait | read | DMA(g,c+1), or at the last chunk DMA(g',0) (g' = next group, or a
+//            harmless reload when there is none: the op count never depends on the group)
 //   end    : argmin, traceback, output stores
+// A two-deep double-buffered variant (kPersistDepth2: DMA of chunk c+2 at chunk c, vmcnt(8)) is
+// SLOWER (persist_bench: 0.306 vs 0.288 ms isolated, 0.365 vs 0.340 sustained; same HBM traffic):
+// the kernel is power-bound (the clock falls from 2.4 GHz without input traffic to 1.9-2.1 GHz
+// with it, profiles/r02_persist_bench.txt), not latency-bound.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -191,7 +192,8 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 }
 
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
-enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4 };
+enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
+             kPersistDepth2 = 16 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -214,7 +216,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   const int nb = a.nblocks;
   const int stride_groups = gridDim.x;
 
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[((ABLATE & kPersistDepth2) ? 2 : 1) * BUF];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   constexpr uint32_t block_bytes = (uint32_t)T * 16;
   // DMA k of a chunk: lane l moves 16-byte unit j = l % 8 of block r = 8k + l / 8 of the group, from
@@ -231,6 +233,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   // Groups holding the batch's last block clamp every unit into the buffer (a lane past the batch
   // replays block nb-1; a unit past the block end re-reads its last step; neither is ever read).
   auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
+    if constexpr ((ABLATE & kPersistCachedInput) != 0) g = blockIdx.x & 7;   // L2-resident input
     if (g * kRegThreads + kRegThreads < nb) {
       const unsigned char* base = in + (size_t)g * kRegThreads * block_bytes + c * PF * 16;
 #pragma unroll
@@ -260,7 +263,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   int g = blockIdx.x;
   if (!(ABLATE & kPersistNoMem) && g < ngroups) {
     issue_chunk(g, 0, 0);
-    issue_chunk(g, 1, 1);
+    if constexpr ((ABLATE & kPersistDepth2) != 0) issue_chunk(g, 1, 1);
   }
   for (; g < ngroups; g += stride_groups) {
     const int b = g * kRegThreads + lane;
@@ -283,11 +286,12 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
           chunk[x] = f32x4{(float)((ln + x) & 3), (float)((ln + x + 1) & 3), (float)((ln + 2 * x) & 3),
                            (float)((ln ^ x) & 3)};
       } else {
-        wait_vmcnt<UPR>();   // this chunk's DMA has landed; the next chunk's may still be in flight
+        if constexpr ((ABLATE & kPersistDepth2) != 0) wait_vmcnt<UPR>();   // the next chunk's may be in flight
+        else wait_vmcnt<0>();
         // row x of this lane's block sits at slot x ^ sw: (row base | sw * 16) ^ (x * 16), the array
         // being 1 KiB aligned
         [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
-          ((chunk[xs] = lds_read_b128<(c % 2) * BUF>(rd_base ^ (uint32_t)(xs * 16))), ...);
+          ((chunk[xs] = lds_read_b128<((ABLATE & kPersistDepth2) ? c % 2 : 0) * BUF>(rd_base ^ (uint32_t)(xs * 16))), ...);
         }(std::make_integer_sequence<int, UPR>{});
         // the rows are in registers once these reads return; only then may the DMA overwrite them
         asm volatile("s_waitcnt lgkmcnt(0)"
@@ -301,8 +305,14 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
           for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
           asm volatile("" ::: "memory");   // keep the info loads before the DMA (issue order above)
         }
-        if constexpr (c + 2 < NCH) issue_chunk(g, c + 2, c % 2);
-        else issue_chunk(has_next ? g + stride_groups : g, c + 2 - NCH, c % 2);
+        if constexpr ((ABLATE & kPersistDepth2) == 0) {
+          if constexpr (c + 1 < NCH) issue_chunk(g, c + 1, 0);
+          else issue_chunk(has_next ? g + stride_groups : g, 0, 0);
+        } else if constexpr (c + 2 < NCH) {
+          issue_chunk(g, c + 2, c % 2);
+        } else {
+          issue_chunk(has_next ? g + stride_groups : g, c + 2 - NCH, c % 2);
+        }
       }
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
         constexpr int t = c * PF + u;

@@ -109,12 +109,15 @@ int main(int argc, char** argv) {
     trace<kK7Ref>(a, ng, 8, cus, n);
     return 0;
   }
-  for (int w : {8, 12}) {
+  for (int w : {8}) {
     run<kK7Ref, 0>("ref full", a, ng, w, cus);
     run<kK7Ref, kPersistNoMem>("ref no-mem", a, ng, w, cus);
     run<kK7Ref, kPersistNoTraceback>("ref no-traceback", a, ng, w, cus);
     run<kK7Ref, kPersistNoMem | kPersistNoTraceback>("ref no-mem no-traceback", a, ng, w, cus);
   }
+  run<kK7Ref, kPersistDepth2>("ref full, 2-deep double-buffered DMA", a, ng, 8, cus);
+  run<kK7Ref, kPersistCachedInput>("ref full, L2-resident input", a, ng, 8, cus);
+  run<kK7Ref, kPersistCachedInput | kPersistNoTraceback>("ref L2 input, no-tb", a, ng, 8, cus);
   run<kK7Ref, kPersistSelectAcs>("ref select-acs full", a, ng, 8, cus);
   run<kK7Ref, kPersistSelectAcs | kPersistNoMem | kPersistNoTraceback>("ref select-acs no-mem no-tb", a, ng, 8, cus);
   run<kK7True, kPersistSelectAcs>("true select-acs full", a, ng, 8, cus);
