@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "acs_persist.hpp"
 #include "acs_reg.hpp"
 #include "trellis.hpp"
 
@@ -130,6 +131,43 @@ __device__ __forceinline__ void multi_acs(MT (&M)[64], const MT (&BM)[1 << C.n],
     if constexpr (R >= 32) hi = shift_in(hi, a0, a1);
     else lo = shift_in(lo, a0, a1);
   }
+}
+
+// Growth step (t = P < K-1, from the reset metrics): the odd predecessor of every state is still
+// unreachable (its candidate is +inf / saturated 0xFF00 and never wins the strict compare), so each
+// new state is its even predecessor plus the branch metric and its decision is 0 -- the adds only
+// (see acs_persist.hpp growth_step; unreachable states stay +inf / 0xFF00 exactly).
+template <CodeSpec C, int P, int R, bool SAT, typename MT>
+__device__ __forceinline__ void multi_growth(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0, bool qb1) {
+  using X = Multi<C>;
+  constexpr int L = X::L;
+  auto sat = [](MT v) {
+    if constexpr (SAT) return vmin(v, (MT)0xFF00);   // binary-symmetric-channel/viterbi-decoder.c:127-130
+    else return v;
+  };
+  if constexpr (P < 6) {
+    if constexpr ((R & (1 << P)) == 0) {
+      constexpr int R1 = R | (1 << P);
+      constexpr auto e = [](int q, int in) { return expected_symbol(C, X::logical(q, R, P), in); };
+      const MT even = M[R];
+      M[R] = sat(even + select_bm<L, e(0, 0), e(1 % L, 0), e(2 % L, 0), e(3 % L, 0)>(BM, qb0, qb1));
+      M[R1] = sat(even + select_bm<L, e(0, 1), e(1 % L, 1), e(2 % L, 1), e(3 % L, 1)>(BM, qb0, qb1));
+    }
+  } else {
+    constexpr int B = P - 6;
+    constexpr int CE = B == 0 ? 0xA0 : 0x44;   // quad_perm [0,0,2,2] / [0,1,0,1]
+    constexpr auto e = [](int q) {
+      const int qe = q & ~(1 << B);
+      return expected_symbol(C, X::logical(qe, R, P), (q >> B) & 1);
+    };
+    M[R] = sat(dpp<CE, MT>(M[R]) + select_bm<L, e(0), e(1 % L), e(2 % L), e(3 % L)>(BM, qb0, qb1));
+  }
+}
+
+template <CodeSpec C, int P, bool SAT, typename MT, size_t... I>
+__device__ __forceinline__ void multi_growth_step_impl(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0,
+                                                       bool qb1, std::index_sequence<I...>) {
+  (multi_growth<C, P, 63 - (int)I, SAT, MT>(M, BM, qb0, qb1), ...);
 }
 
 template <CodeSpec C, int P, bool SAT, typename MT, size_t... I>
@@ -414,6 +452,144 @@ void viterbi_multi_regdec(RegArgs a) {
       errors = (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
     }
   }
+  accumulate_errors(a, errors);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent K = 9 soft kernel at the codebook block length (blen 40: T = 48 = six periods of the
+// 8-phase rotation, so a period is exactly one 8-step input chunk), built like the K <= 7
+// persistent kernel (acs_persist.hpp): resident waves walk groups of 16 blocks (4 lanes each);
+// period 0 is the growth from the reset metrics (adds only, no decisions); the 40 main steps keep
+// their decision words in VGPRs; the input is staged by LDS-DMA one chunk ahead (2 KiB per chunk:
+// 16 blocks x 8 steps x 16 bytes; the 4 lanes of a block read the same row).
+template <CodeSpec C, int BLEN>
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void viterbi_multi_persist(RegArgs a, int ngroups) {
+  using X = Multi<C>;
+  using MT = float;
+  static_assert(C.K == 9 && C.n == 2, "K = 9, r = 1/2: the period (8 steps) is the 8-step chunk");
+  constexpr int n = X::n;                     // 8 phases per period
+  constexpr int T = BLEN + C.K - 1;
+  static_assert(T % n == 0 && T / n >= 2 && T / n <= 7, "whole periods");
+  constexpr int NPER = T / n;                 // periods = chunks
+  constexpr int NMAIN = NPER - 1;             // periods with decisions
+  constexpr int BPG = kRegThreads / X::L;     // blocks per group (16)
+  constexpr int ROWB = n * 16;                // one chunk of one block: 128 bytes
+  constexpr int BUF = BPG * ROWB;             // 2 KiB
+  constexpr int UNITS = BUF / 16;             // 16-byte DMA units per chunk (128: 2 instructions)
+  constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
+  constexpr uint32_t block_bytes = (uint32_t)T * 16;
+  const int lane = threadIdx.x;
+  const int q = lane & (X::L - 1);
+  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
+  const int nb = a.nblocks;
+  const int stride_groups = gridDim.x;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[BUF];
+  const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
+  // DMA k of a chunk: unit k*64 + lane = block r (of 16), 16-byte step j of its chunk
+  auto issue_chunk = [&](int g, int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < UNITS / kRegThreads; ++k) {
+      const int unit = k * kRegThreads + lane;
+      const int r = unit / n, j = unit % n;
+      const int gb = g * BPG + r < nb ? g * BPG + r : nb - 1;
+      __builtin_amdgcn_global_load_lds(in + (size_t)gb * block_bytes + (uint32_t)(c * n + j) * 16,
+                                       (lds_ptr_t)(lds + k * kRegThreads * 16), 16, 0, 0);
+    }
+  };
+  const uint32_t row = (uint32_t)(uintptr_t)(lds_ptr_t)lds + (uint32_t)((lane / X::L) * ROWB);
+  const uint8_t* info_src = a.info != nullptr ? a.info : reinterpret_cast<const uint8_t*>(a.in);
+  const int info_stride = a.info != nullptr ? IB : 0;
+  const int gbase = lane & ~(X::L - 1);
+
+  uint32_t errors = 0;
+  int g = blockIdx.x;
+  if (g < ngroups) issue_chunk(g, 0);
+  for (; g < ngroups; g += stride_groups) {
+    const int blk = g * BPG + lane / X::L;
+    const bool has_next = g + stride_groups < ngroups;
+    MT M[64];
+#pragma unroll
+    for (int r = 0; r < 64; ++r) M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
+    uint64_t D[NMAIN][n];
+    uint8_t info[IB];
+    auto period_at = [&]<int p>() __attribute__((always_inline)) {
+      f32x4 chunk[n];
+      wait_vmcnt<0>();
+      [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
+        ((chunk[xs] = lds_read_b128<xs * 16>(row)), ...);
+      }(std::make_integer_sequence<int, n>{});
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(chunk[0]), "+v"(chunk[1]), "+v"(chunk[2]), "+v"(chunk[3]), "+v"(chunk[4]),
+                     "+v"(chunk[5]), "+v"(chunk[6]), "+v"(chunk[7])
+                   :
+                   : "memory");
+      if constexpr (p == 0) {
+        const int bc = blk < nb ? blk : nb - 1;
+#pragma unroll
+        for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
+        asm volatile("" ::: "memory");   // info loads before the DMA (vmcnt order)
+      }
+      if constexpr (p + 1 < NPER) issue_chunk(g, p + 1);
+      else issue_chunk(has_next ? g + stride_groups : g, 0);
+      auto phase_at = [&]<int P>() __attribute__((always_inline)) {
+        const MT BM[4] = {chunk[P].x, chunk[P].y, chunk[P].z, chunk[P].w};
+        if constexpr (p == 0) {
+          multi_growth_step_impl<C, P, false, MT>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
+        } else {
+          D[p - 1][P] = multi_step<C, P, false, MT>(M, BM, qb0, qb1);
+          pin(D[p - 1][P]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
+        (phase_at.template operator()<Ps>(), ...);
+      }(std::make_integer_sequence<int, n>{});
+    };
+    [&]<int... ps>(std::integer_sequence<int, ps...>) __attribute__((always_inline)) {
+      (period_at.template operator()<ps>(), ...);
+    }(std::make_integer_sequence<int, NPER>{});
+
+    MT best;
+    uint32_t st = multi_argmin<C, MT>(M, T % n, q, (MT)__builtin_inff(), best);
+    uint64_t bits = 0;
+    auto back_step = [&]<int p, int P>() __attribute__((always_inline)) {
+      // survivors of step t sit at the phase-(t+1) positions (t mod n = P)
+      const uint32_t phys = rotl_bits(st, P + 1 == n ? 0 : P + 1, n);
+      uint32_t bit = 0;
+      if constexpr (p > 0) {
+        const uint32_t pos = multi_dec_pos(phys & 63u, P);
+        const uint64_t w = D[p - 1][P];
+        const uint32_t half = pos < 32 ? (uint32_t)w : (uint32_t)(w >> 32);
+        const int src = (gbase + (int)(phys >> 6)) << 2;
+        const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)half);
+        bit = (word >> (pos & 31)) & 1u;
+      }
+      bits = (bits >> 1) | ((uint64_t)(st >> (C.K - 2)) << 63);
+      st = ((st << 1) & (X::S - 1)) | bit;
+    };
+    auto back_period = [&]<int p>() __attribute__((always_inline)) {
+      [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
+        (back_step.template operator()<p, n - 1 - Ps>(), ...);
+      }(std::make_integer_sequence<int, n>{});
+    };
+    [&]<int... ps>(std::integer_sequence<int, ps...>) __attribute__((always_inline)) {
+      (back_period.template operator()<NPER - 1 - ps>(), ...);
+    }(std::make_integer_sequence<int, NPER>{});
+    if (q == 0 && blk < nb) {
+      uint8_t* o = a.out + (size_t)blk * OB;
+#pragma unroll
+      for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
+      if (a.info != nullptr) {   // consumer AWGN-channel/main.c:118-144
+        uint64_t ref = 0;
+#pragma unroll
+        for (int k = 0; k < IB; ++k) ref |= (uint64_t)info[k] << (56 - 8 * k);
+        constexpr uint64_t mask = BLEN >= 64 ? ~0ull : ~(~0ull >> BLEN);
+        errors += (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
+      }
+    }
+  }
+  wait_vmcnt<0>();   // the look-ahead DMA writes LDS: it must land before the workgroup ends
   accumulate_errors(a, errors);
 }
 

@@ -120,9 +120,12 @@ ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
 // The persistent K <= 7 kernel (acs_persist.hpp), or nullptr: codebook block length, block-major
 // input, decisions not exported.
 ccv::RegLaunchFn persist_kernel(const ccv_plan& p, bool export_decisions) {
-  if (p.no_persistent || p.global_decisions || export_decisions || p.reg_index < 0 || p.step_major ||
+  if (p.no_persistent || p.global_decisions || export_decisions || p.step_major ||
       p.d.blen != ccv::kPersistBlen)
     return nullptr;
+  if (p.multi_index >= 0)
+    return p.d.channel == CCV_SOFT ? ccv::multi_persist_launchers()[p.multi_index] : nullptr;
+  if (p.reg_index < 0) return nullptr;
   return ccv::persist_launchers(p.d.channel == CCV_HARD)[p.reg_index];
 }
 
@@ -366,8 +369,10 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     a.info = d_info;
     a.err = d_info ? d_errors : nullptr;
     if (const ccv::RegLaunchFn persist = persist_kernel(*p, d_decisions != nullptr)) {
-      // decisions in VGPRs, grid = resident waves walking 64-block groups (acs_persist.hpp)
-      const size_t full = nblocks / ccv::kRegThreads, rem = nblocks % ccv::kRegThreads;
+      // decisions in VGPRs, grid = resident waves walking groups of 64 / lanes blocks
+      // (acs_persist.hpp, acs_multi.hpp)
+      const size_t per_group = ccv::kRegThreads / (size_t)p->d.lanes;
+      const size_t full = nblocks / per_group, rem = nblocks % per_group;
       if (!hard) {
         HIP_TRY(persist(a, (int)(full + (rem ? 1 : 0)), stream));
         return 0;

@@ -61,6 +61,10 @@ const RegLaunchFn* multi_launchers(bool hard);   // [kNumMultiCodes], reg_multi.
 // T <= multi_regdec_max_steps(K) and no decision export (reg_multi.hip)
 const RegLaunchFn* multi_regdec_launchers(bool hard);
 int multi_regdec_max_steps(int K);
+// [kNumMultiCodes] persistent soft kernel (acs_multi.hpp viterbi_multi_persist; int argument =
+// groups of 64 / 2^(K-7) blocks), nullptr where a code has none (K = 9, r = 1/2 only); valid for
+// blen == kPersistBlen, block-major input, no decision export (reg_multi.hip)
+const RegLaunchFn* multi_persist_launchers();
 
 struct ChanArgs;
 using ChanLaunchFn = hipError_t (*)(const ChanArgs&, int grid, hipStream_t stream);

@@ -34,7 +34,21 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_regdec(std::index_sequence<
   return {&launch_regdec<I, HARD>...};
 }
 
+template <size_t I>
+hipError_t launch_persist(const RegArgs& a, int ngroups, hipStream_t stream) {
+  if constexpr (kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2)
+    return launch_persistent(viterbi_multi_persist<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
+  else
+    return hipErrorInvalidValue;
+}
+
+template <size_t... I>
+constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence<I...>) {
+  return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2) ? &launch_persist<I> : nullptr)...};
+}
+
 constexpr auto kSoft = make<false>(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kSoftPersist = make_persist(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kHard = make<true>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kSoftRegDec = make_regdec<false>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kHardRegDec = make_regdec<true>(std::make_index_sequence<kNumMultiCodes>{});
@@ -42,6 +56,8 @@ constexpr auto kHardRegDec = make_regdec<true>(std::make_index_sequence<kNumMult
 }  // namespace
 
 const RegLaunchFn* multi_launchers(bool hard) { return hard ? kHard.data() : kSoft.data(); }
+
+const RegLaunchFn* multi_persist_launchers() { return kSoftPersist.data(); }
 
 const RegLaunchFn* multi_regdec_launchers(bool hard) {
   return hard ? kHardRegDec.data() : kSoftRegDec.data();
