@@ -142,9 +142,11 @@ def main():
                     help="k7 (default), k9, k15 (stack default), code0..code5; suffix :true = true parity")
     ap.add_argument("--decoder", choices=("viterbi", "stack", "fano"), default="viterbi",
                     help="viterbi (BASELINE configs 1-4), the stack decoder (config 5, K=15) or Fano")
-    ap.add_argument("--frames", type=int, default=64,
-                    help="1 M-bit frames per GPU per step (64 = 1.6 M blocks = 25,000 one-wave tiles, "
-                         "~6 waves per SIMD so the last partial round is a small fraction)")
+    ap.add_argument("--frames", type=int, default=104,
+                    help="1 M-bit frames per GPU per step. 104 = 2.6 M blocks = 40,625 groups of 64 "
+                         "blocks for the 2,048 resident waves of the persistent K=7 kernel: 19.8 groups "
+                         "each, so the last, partial round of groups idles <1%% of the waves (64 frames: "
+                         "12.2 groups each, 6%%)")
     ap.add_argument("--ebn0", type=float, default=4.0)
     ap.add_argument("--channel", choices=("awgn", "bsc"), default="awgn",
                     help="awgn: soft decision (configs 2, 3, 5); bsc: hard decision (configs 1, 4)")

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_traffic
 mkdir -p $OUT
-ARGS="${*:---code k7 --frames 64 --layout block}"
+ARGS="${*:---code k7 --frames 104 --layout block}"
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d $OUT/$ctr -o run -- \
       python tools/traffic_probe.py $ARGS > $OUT/$ctr.log 2>&1 || { tail -20 $OUT/$ctr.log; exit 1; }
