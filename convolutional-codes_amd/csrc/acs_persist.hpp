@@ -194,7 +194,7 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
-             kPersistDepth2 = 16 };
+             kPersistDepth2 = 16, kPersistLineChunks = 32 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -212,12 +212,25 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
   static_assert(BLEN >= 1 && BLEN <= kPersistMaxMain, "decisions of the main steps live in VGPRs");
   static_assert(NCH >= 4 && NCH % 2 == 0, "buffer = chunk parity across groups");
+  // Line-aligned staging (LINES, ablation kPersistLineChunks): block r of a group starts
+  // phi_r = r*T mod 8 steps into a 128-byte line, so its 8-step chunks straddle two lines and a line
+  // is fetched twice whenever the L2 dropped it between two chunks (PMC: 2.63 GB per launch for
+  // 1.91 GB of input; a line-aligned input (blen 42, T = 48) fetches 25 % less and keeps a higher
+  // clock). LINES instead has DMA k move block r's k-th ALIGNED line (steps 8k - phi_r ..; NCH + 1
+  // lines), two line buffers alternate, and window w reads each lane's steps from lines w and w + 1
+  // at lane-dependent slots. Bit-exact, 10 % less fetch (the line a block shares with the next is
+  // still fetched twice), but slower (persist_bench 0.345 vs 0.295 ms; profiles/r02_persist_bench.txt):
+  // not the production path.
+  constexpr bool LINES = (T % PF) != 0 && (ABLATE & kPersistLineChunks) != 0 &&
+                         (ABLATE & (kPersistNoMem | kPersistDepth2)) == 0;
+  constexpr int NLINE = NCH + 1;              // aligned lines per block window sequence (LINES)
   using DW = DecWord<S>;
   const int lane = threadIdx.x;
   const int nb = a.nblocks;
   const int stride_groups = gridDim.x;
 
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[((ABLATE & kPersistDepth2) ? 2 : 1) * BUF];
+  __shared__ __attribute__((aligned(1024))) unsigned char
+      lds[(LINES || (ABLATE & kPersistDepth2)) ? 2 * BUF : BUF];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   constexpr uint32_t block_bytes = (uint32_t)T * 16;
   // DMA k of a chunk: lane l moves 16-byte unit j = l % 8 of block r = 8k + l / 8 of the group, from
@@ -229,8 +242,42 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   for (int k = 0; k < UPR; ++k) {
     const int r = k * (kRegThreads / UPR) + lane / UPR, j = lane % UPR;
     const int su = j ^ ((r / GRP) % UPR);
-    dma_off[k] = (uint32_t)r * block_bytes + (uint32_t)su * 16;
+    if constexpr (LINES) dma_off[k] = (((uint32_t)r * (uint32_t)T) >> 3) * 128 + (uint32_t)su * 16;
+    else dma_off[k] = (uint32_t)r * block_bytes + (uint32_t)su * 16;
   }
+  // LINES: the line DMA; groups holding the batch's last block clamp each unit into the buffer
+  const size_t total_bytes = (size_t)nb * block_bytes;
+  auto issue_line = [&](int g, int k, int buf) __attribute__((always_inline)) {
+    const size_t gbase = (size_t)g * kRegThreads * block_bytes;
+    if (g * kRegThreads + kRegThreads < nb) {
+      const unsigned char* base = in + gbase + k * 128;
+#pragma unroll
+      for (int kk = 0; kk < UPR; ++kk)
+        __builtin_amdgcn_global_load_lds(base + dma_off[kk], (lds_ptr_t)(lds + buf * BUF + kk * kRegThreads * 16),
+                                         16, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < UPR; ++kk) {
+        size_t off = gbase + (size_t)k * 128 + dma_off[kk];
+        off = off + 16 <= total_bytes ? off : total_bytes - 16;
+        __builtin_amdgcn_global_load_lds(in + off, (lds_ptr_t)(lds + buf * BUF + kk * kRegThreads * 16), 16, 0, 0);
+      }
+    }
+  };
+  // LINES: byte offset (inside the two-buffer LDS block) of this lane's step x of a window, for
+  // window parity 0 (bit 13 = which buffer); odd windows flip bit 13
+  // (two 14-bit offsets per VGPR: 4 registers, where the K=7 true-parity build has none to spare)
+  uint32_t rd_pk[UPR / 2];
+  {
+    const int phi = (lane * T) & 7, sw = (lane / GRP) % UPR;
+#pragma unroll
+    for (int x = 0; x < UPR; x += 2) {
+      const uint32_t o0 = (uint32_t)(((x + phi) >> 3) * BUF + lane * ROWB + ((((x + phi) & 7) ^ sw) << 4));
+      const uint32_t o1 = (uint32_t)(((x + 1 + phi) >> 3) * BUF + lane * ROWB + ((((x + 1 + phi) & 7) ^ sw) << 4));
+      rd_pk[x / 2] = o0 | (o1 << 16);
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)lds;
   // Groups holding the batch's last block clamp every unit into the buffer (a lane past the batch
   // replays block nb-1; a unit past the block end re-reads its last step; neither is ever read).
   auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
@@ -262,11 +309,17 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
 
   uint32_t errors = 0;
   int g = blockIdx.x;
+  uint32_t gp = 0;   // LINES: buffer of the group's line 0 (flips per group: NLINE is odd)
   if (!(ABLATE & kPersistNoMem) && g < ngroups) {
-    issue_chunk(g, 0, 0);
-    if constexpr ((ABLATE & kPersistDepth2) != 0) issue_chunk(g, 1, 1);
+    if constexpr (LINES) {
+      issue_line(g, 0, 0);
+      issue_line(g, 1, 1);
+    } else {
+      issue_chunk(g, 0, 0);
+      if constexpr ((ABLATE & kPersistDepth2) != 0) issue_chunk(g, 1, 1);
+    }
   }
-  for (; g < ngroups; g += stride_groups) {
+  for (; g < ngroups; g += stride_groups, gp ^= (NLINE & 1)) {
     const int b = g * kRegThreads + lane;
     const bool has_next = g + stride_groups < ngroups;
     float M[S];
@@ -286,6 +339,39 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
         for (int x = 0; x < UPR; ++x)
           chunk[x] = f32x4{(float)((ln + x) & 3), (float)((ln + x + 1) & 3), (float)((ln + 2 * x) & 3),
                            (float)((ln ^ x) & 3)};
+      } else if constexpr (LINES) {
+        wait_vmcnt<0>();   // lines c and c + 1 have landed
+        const uint32_t flip = ((c + gp) & 1) * BUF;
+        uint32_t pk[UPR / 2];
+#pragma unroll
+        for (int i = 0; i < UPR / 2; ++i) {
+          pk[i] = rd_pk[i];
+          asm volatile("" : "+v"(pk[i]));   // unpack here, not once for the whole kernel
+        }
+        [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
+          ((chunk[xs] = lds_read_b128<0>(lds0 + (((xs & 1) ? (pk[xs / 2] >> 16) : (pk[xs / 2] & 0xFFFFu)) ^ flip))),
+           ...);
+        }(std::make_integer_sequence<int, UPR>{});
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(chunk[0]), "+v"(chunk[1]), "+v"(chunk[2]), "+v"(chunk[3]), "+v"(chunk[4]),
+                       "+v"(chunk[5]), "+v"(chunk[6]), "+v"(chunk[7])
+                     :
+                     : "memory");
+        if constexpr (c == 0) {
+          const int bc = b < nb ? b : nb - 1;
+#pragma unroll
+          for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
+          asm volatile("" ::: "memory");
+        }
+        // line c is consumed by every lane: its buffer takes line c + 2, or, after the last window,
+        // both buffers take lines 0 and 1 of the next group (whose line 0 lands in buffer gp ^ 1)
+        if constexpr (c + 2 < NLINE) {
+          issue_line(g, c + 2, (int)((c + gp) & 1));
+        } else {
+          const int gn = has_next ? g + stride_groups : g;
+          issue_line(gn, 0, (int)(gp ^ (NLINE & 1)));
+          issue_line(gn, 1, (int)(gp ^ (NLINE & 1) ^ 1));
+        }
       } else {
         if constexpr ((ABLATE & kPersistDepth2) != 0) wait_vmcnt<UPR>();   // the next chunk's may be in flight
         else wait_vmcnt<0>();

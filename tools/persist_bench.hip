@@ -24,9 +24,9 @@ constexpr CodeSpec kK7True{2, 7, {0xF200000000000000ull, 0xB600000000000000ull, 
     }                                                                         \
   } while (0)
 
-template <CodeSpec C, int AB>
+template <CodeSpec C, int AB, int BLEN = 40>
 int run(const char* name, RegArgs a, int ngroups, int waves_per_cu, int cus) {
-  auto kern = viterbi_soft_persist<C, 40, AB>;
+  auto kern = viterbi_soft_persist<C, BLEN, AB>;
   int per_cu = 0;
   CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
   const int w = waves_per_cu < per_cu ? waves_per_cu : per_cu;
@@ -52,7 +52,7 @@ int run(const char* name, RegArgs a, int ngroups, int waves_per_cu, int cus) {
   float sus = 0;
   CHECK(hipEventElapsedTime(&sus, e0, e1));
   sus /= 40;
-  const double bits = (double)ngroups * 64 * 40;
+  const double bits = (double)ngroups * 64 * BLEN;
   printf("%-28s waves/CU %2d (max %2d)  isolated %.4f ms %6.1f Gbit/s  sustained %.4f ms %6.1f Gbit/s\n",
          name, w, per_cu, best, bits / (best * 1e-3) / 1e9, sus, bits / (sus * 1e-3) / 1e9);
   return 0;
@@ -115,7 +115,17 @@ int main(int argc, char** argv) {
     run<kK7Ref, kPersistNoTraceback>("ref no-traceback", a, ng, w, cus);
     run<kK7Ref, kPersistNoMem | kPersistNoTraceback>("ref no-mem no-traceback", a, ng, w, cus);
   }
+  run<kK7Ref, kPersistLineChunks>("ref full, line-aligned chunks", a, ng, 8, cus);
   run<kK7Ref, kPersistDepth2>("ref full, 2-deep double-buffered DMA", a, ng, 8, cus);
+  {   // blen 42: T = 48, a block is exactly 6 x 128-byte lines -> no chunk straddles a line
+    RegArgs a42 = a;
+    a42.T = 48;
+    a42.blen = 42;
+    const int nb42 = (int)((size_t)nb * 46 / 48) / 64 * 64;   // same input bytes
+    a42.nblocks = nb42;
+    run<kK7Ref, 0, 42>("ref full blen42 (aligned)", a42, nb42 / 64, 8, cus);
+    run<kK7Ref, kPersistCachedInput, 42>("ref blen42 L2-resident", a42, nb42 / 64, 8, cus);
+  }
   run<kK7Ref, kPersistCachedInput>("ref full, L2-resident input", a, ng, 8, cus);
   run<kK7Ref, kPersistCachedInput | kPersistNoTraceback>("ref L2 input, no-tb", a, ng, 8, cus);
   run<kK7Ref, kPersistSelectAcs>("ref select-acs full", a, ng, 8, cus);
