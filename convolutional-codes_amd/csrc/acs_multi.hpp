@@ -236,6 +236,35 @@ __device__ __forceinline__ uint32_t multi_argmin(const MT (&M)[64], int phase, i
   return idx == 0xFFFFFFFFu ? 0u : idx;   // nothing below the sentinel: state 0 as the reference
 }
 
+// Same, for a trellis that ends on phase 0 (T % n == 0: the persistent kernels), without the
+// compare/select chain (acs_reg.hpp argmin_state): the logical index is (q << 6) | r, so the answer
+// is the lowest lane holding the group's minimum and, in it, the lowest register. v_min3 tree,
+// lane minimum, "differs" mask from the sign of min - M[r], lowest clear bit, lane minimum.
+template <CodeSpec C>
+__device__ __forceinline__ uint32_t multi_argmin_phase0(const float (&M)[64], int q, float sentinel,
+                                                        float& best) {
+  using X = Multi<C>;
+  float mn = tree_min<64, float>(M);
+#pragma unroll
+  for (int off = 1; off < X::L; off <<= 1) mn = vmin(mn, __shfl_xor(mn, off, 64));
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int r = 31; r >= 0; --r) {
+    lo = __builtin_amdgcn_alignbit(lo, min_minus(mn, M[r]), 31);
+    hi = __builtin_amdgcn_alignbit(hi, min_minus(mn, M[r + 32]), 31);
+  }
+  const uint64_t eq = ~(((uint64_t)hi << 32) | lo);
+  uint32_t idx = eq ? (((uint32_t)q << 6) | (uint32_t)__builtin_ctzll(eq)) : 0xFFFFFFFFu;
+#pragma unroll
+  for (int off = 1; off < X::L; off <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)idx, off, 64);
+    idx = o < idx ? o : idx;
+  }
+  const bool found = mn < sentinel;   // nothing below the sentinel: state 0, as the reference
+  best = found ? mn : sentinel;
+  return found ? idx : 0u;
+}
+
 template <CodeSpec C>
 __device__ __forceinline__ uint32_t multi_traceback(const RegArgs& a, int blk, uint32_t st, bool writer) {
   using X = Multi<C>;
@@ -551,7 +580,8 @@ void viterbi_multi_persist(RegArgs a, int ngroups) {
     }(std::make_integer_sequence<int, NPER>{});
 
     MT best;
-    uint32_t st = multi_argmin<C, MT>(M, T % n, q, (MT)__builtin_inff(), best);
+    static_assert(T % n == 0, "the persistent trellis ends on phase 0");
+    uint32_t st = multi_argmin_phase0<C>(M, q, __builtin_inff(), best);
     uint64_t bits = 0;
     auto back_step = [&]<int p, int P>() __attribute__((always_inline)) {
       // survivors of step t sit at the phase-(t+1) positions (t mod n = P)

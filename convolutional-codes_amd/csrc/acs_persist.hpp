@@ -117,25 +117,34 @@ __device__ __forceinline__ void growth_step(MT (&M)[1 << (C.K - 1)], const MT (&
 // 0 on every path through them). Returns the T decoded bits MSB-aligned: bit 63 = step 0.
 // F_rt == F at run time: the per-8-step guards only cut the code into basic blocks (a fully
 // straight-line kernel makes the register allocator spill thousands of VGPRs; see acs_persist notes).
+// The output bit of step t is the top bit of the state there, and walking back shifts each decision in
+// at the bottom of the state: so the output bits of steps T-1 .. 0 are the final state's K-1 bits
+// followed by the decisions read at main steps F-1 .. 0, and one history word h (low K-1 bits = the
+// current state) carries the whole traceback: d = D[m] >> (h mod S) (for K = 6, 7 the mask is the
+// shifter's own), h = (h << 1) | (d & 1) -- three VALU ops per step. The history
+// outgrows 32 bits after 33 - K steps: the word is saved then and the walk continues in the low bits.
 template <int K, typename DW, int F>
 __device__ __forceinline__ uint64_t traceback_regs(const DW (&D)[F], uint32_t st, int F_rt) {
   constexpr int S = 1 << (K - 1);
-  uint64_t bits = 0;
+  constexpr int T = F + K - 1;
+  static_assert(T <= 64, "history fits two words");
+  constexpr int SPLIT = 33 - K;   // main steps after which h holds 32 bits
+  uint32_t h = st, hi = 0;
 #pragma unroll
-  for (int m = F - 1; m >= 0; --m) {
+  for (int j = 0; j < F; ++j) {
+    const int m = F - 1 - j;
     if (m % 8 == 7 || m == F - 1) {
       if (m >= F_rt) continue;
     }
-    const uint32_t d = (uint32_t)(D[m] >> st) & 1u;
-    bits = (bits >> 1) | ((uint64_t)(st >> (K - 2)) << 63);
-    st = ((st << 1) & (S - 1)) | d;
+    const uint32_t d = (uint32_t)(D[m] >> (h & (S - 1)));   // the mask folds into the shifter
+    h = (h << 1) | (d & 1u);
+    if (j + 1 == SPLIT) hi = h;
   }
-#pragma unroll
-  for (int g = 0; g < K - 1; ++g) {
-    bits = (bits >> 1) | ((uint64_t)(st >> (K - 2)) << 63);
-    st = (st << 1) & (S - 1);
-  }
-  return bits;
+  // bit i of H = output of step i
+  uint64_t H;
+  if constexpr (F <= SPLIT) H = h;
+  else H = ((uint64_t)hi << (F - SPLIT)) | (h & ((1u << (F - SPLIT)) - 1u));
+  return __builtin_bitreverse64(H);   // bit 63 - t = output of step t
 }
 
 // Output bytes (MSB-first, reference traceback :88) and the bit errors of the first blen bits
@@ -174,10 +183,11 @@ __device__ __forceinline__ uint64_t load_info(const RegArgs& a, int b) {
 //   chunk c: wait | read | DMA(g,c+1), or at the last chunk DMA(g',0) (g' = next group, or a
 //            harmless reload when there is none: the op count never depends on the group)
 //   end    : argmin, traceback, output stores
-// A two-deep double-buffered variant (kPersistDepth2: DMA of chunk c+2 at chunk c, vmcnt(8)) is
-// SLOWER (persist_bench: 0.306 vs 0.288 ms isolated, 0.365 vs 0.340 sustained; same HBM traffic):
-// the kernel is power-bound (the clock falls from 2.4 GHz without input traffic to 1.9-2.1 GHz
-// with it, profiles/r02_persist_bench.txt), not latency-bound.
+// Two chunks in flight in two buffers (kPersistDepth2: DMA of chunk c+2 at chunk c, vmcnt(8), which
+// is exact because loads complete in order and at most OB < 8 stores sit between) is no faster:
+// 1.005x the time in paired ABBA runs (tools/persist_bench ab, profiles/r02_persist_ab.txt). The
+// kernel is power-bound (the clock falls from 2.4 GHz without input traffic to 1.9-2.1 GHz with
+// it, profiles/r02_persist_bench.txt), not latency-bound.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -194,7 +204,8 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
-             kPersistDepth2 = 16, kPersistLineChunks = 32 };
+             kPersistDepth2 = 16, kPersistLineChunks = 32, kPersistNoMemRandom = 64,
+             kPersistNoDma = 128, kPersistNoLdsRead = 256 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -221,8 +232,8 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   // at lane-dependent slots. Bit-exact, 10 % less fetch (the line a block shares with the next is
   // still fetched twice), but slower (persist_bench 0.345 vs 0.295 ms; profiles/r02_persist_bench.txt):
   // not the production path.
-  constexpr bool LINES = (T % PF) != 0 && (ABLATE & kPersistLineChunks) != 0 &&
-                         (ABLATE & (kPersistNoMem | kPersistDepth2)) == 0;
+  constexpr bool LINES = (T % PF) != 0 && (ABLATE & kPersistLineChunks) != 0 && (ABLATE & kPersistNoMem) == 0;
+  constexpr bool DEPTH2 = !LINES && (ABLATE & kPersistDepth2) != 0;   // two chunks in flight
   constexpr int NLINE = NCH + 1;              // aligned lines per block window sequence (LINES)
   using DW = DecWord<S>;
   const int lane = threadIdx.x;
@@ -230,7 +241,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   const int stride_groups = gridDim.x;
 
   __shared__ __attribute__((aligned(1024))) unsigned char
-      lds[(LINES || (ABLATE & kPersistDepth2)) ? 2 * BUF : BUF];
+      lds[(LINES || DEPTH2) ? 2 * BUF : BUF];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   constexpr uint32_t block_bytes = (uint32_t)T * 16;
   // DMA k of a chunk: lane l moves 16-byte unit j = l % 8 of block r = 8k + l / 8 of the group, from
@@ -281,6 +292,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   // Groups holding the batch's last block clamp every unit into the buffer (a lane past the batch
   // replays block nb-1; a unit past the block end re-reads its last step; neither is ever read).
   auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
+    if constexpr ((ABLATE & kPersistNoDma) != 0) return;   // ablation: LDS reads of stale rows
     if constexpr ((ABLATE & kPersistCachedInput) != 0) g = blockIdx.x & 7;   // L2-resident input
     if (g * kRegThreads + kRegThreads < nb) {
       const unsigned char* base = in + (size_t)g * kRegThreads * block_bytes + c * PF * 16;
@@ -316,7 +328,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
       issue_line(g, 1, 1);
     } else {
       issue_chunk(g, 0, 0);
-      if constexpr ((ABLATE & kPersistDepth2) != 0) issue_chunk(g, 1, 1);
+      if constexpr (DEPTH2) issue_chunk(g, 1, 1);
     }
   }
   for (; g < ngroups; g += stride_groups, gp ^= (NLINE & 1)) {
@@ -332,7 +344,20 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
     // its steps
     auto chunk_at = [&]<int c>() __attribute__((always_inline)) {
       f32x4 chunk[UPR];
-      if constexpr ((ABLATE & kPersistNoMem) != 0) {
+      // ablations: full-entropy synthetic rows in [1, 2) instead of LDS reads
+      auto synth_rows = [&]() __attribute__((always_inline)) {
+        uint32_t ln = (uint32_t)(lane + g) * 0x9E3779B9u;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int x = 0; x < UPR; ++x) {
+          const uint32_t r0 = ln ^ (uint32_t)(x * 0x85EBCA6Bu), r1 = r0 * 0xC2B2AE35u;
+          chunk[x] = f32x4{__uint_as_float((r0 >> 9) | 0x3F800000u), __uint_as_float((r1 >> 9) | 0x3F800000u),
+                           __uint_as_float((r0 & 0x7FFFFFu) | 0x3F800000u), __uint_as_float((r1 & 0x7FFFFFu) | 0x3F800000u)};
+        }
+      };
+      if constexpr ((ABLATE & kPersistNoMemRandom) != 0) {   // no memory, full-entropy values
+        synth_rows();
+      } else if constexpr ((ABLATE & kPersistNoMem) != 0) {
         int ln = lane + g;
         asm volatile("" : "+v"(ln));
 #pragma unroll
@@ -373,12 +398,13 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
           issue_line(gn, 1, (int)(gp ^ (NLINE & 1) ^ 1));
         }
       } else {
-        if constexpr ((ABLATE & kPersistDepth2) != 0) wait_vmcnt<UPR>();   // the next chunk's may be in flight
+        if constexpr (DEPTH2) wait_vmcnt<UPR>();   // the next chunk's may be in flight
         else wait_vmcnt<0>();
         // row x of this lane's block sits at slot x ^ sw: (row base | sw * 16) ^ (x * 16), the array
         // being 1 KiB aligned
-        [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
-          ((chunk[xs] = lds_read_b128<((ABLATE & kPersistDepth2) ? c % 2 : 0) * BUF>(rd_base ^ (uint32_t)(xs * 16))), ...);
+        if constexpr ((ABLATE & kPersistNoLdsRead) != 0) synth_rows();
+        else [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
+          ((chunk[xs] = lds_read_b128<(DEPTH2 ? c % 2 : 0) * BUF>(rd_base ^ (uint32_t)(xs * 16))), ...);
         }(std::make_integer_sequence<int, UPR>{});
         // the rows are in registers once these reads return; only then may the DMA overwrite them
         asm volatile("s_waitcnt lgkmcnt(0)"
@@ -392,7 +418,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
           for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
           asm volatile("" ::: "memory");   // keep the info loads before the DMA (issue order above)
         }
-        if constexpr ((ABLATE & kPersistDepth2) == 0) {
+        if constexpr (!DEPTH2) {
           if constexpr (c + 1 < NCH) issue_chunk(g, c + 1, 0);
           else issue_chunk(has_next ? g + stride_groups : g, 0, 0);
         } else if constexpr (c + 2 < NCH) {

@@ -220,18 +220,62 @@ struct RegArgs {
 
 constexpr int kRegThreads = 64;   // one wave per workgroup: spreads small batches over more CUs
 
-// Lowest-index minimum (reference traceback :72-79, strict < from the sentinel).
+// Lowest-index minimum (reference traceback :72-79, strict < from the sentinel) without a
+// compare/select chain: hipcc turns `lt = M[s] < best; best = lt ? ..; idx = lt ? ..` into
+// v_cmp -> VCC -> two v_cndmask per state, ~20 ns per state per SIMD on gfx950 (VCC round trip,
+// tools/raterbench6.hip) -- as much as seven K=7 ACS steps per block. Instead: a v_min3 tree for the
+// minimum mn, then per state the sign of mn - M[s] -- 0 exactly when M[s] == mn -- shifted into a
+// "differs" mask (one v_sub and one v_alignbit per state), whose lowest clear bit is the state.
+// mn - M[s] is +0 on equality because path metrics are never -0 (sums that start from the +0 reset
+// metric: x + y is -0 only when both are) and never NaN (finite inputs); a larger M[s], +inf
+// included, gives a negative difference. Hard metrics are u32 below 2^31: the integer difference.
+__device__ __forceinline__ uint32_t min_minus(float mn, float m) { return __float_as_uint(mn - m); }
+__device__ __forceinline__ uint32_t min_minus(uint32_t mn, uint32_t m) { return mn - m; }
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t vmin3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+template <int N, typename MT>
+__device__ __forceinline__ MT tree_min(const MT* v) {
+  if constexpr (N == 1) return v[0];
+  else if constexpr (N == 2) return vmin(v[0], v[1]);
+  else {
+    constexpr int P = (N + 2) / 3;   // parents: min3 over triples, a ragged tail as min / copy
+    MT p[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      if (3 * i + 2 < N) p[i] = vmin3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
+      else if (3 * i + 1 < N) p[i] = vmin(v[3 * i], v[3 * i + 1]);
+      else p[i] = v[3 * i];
+    }
+    return tree_min<P, MT>(p);
+  }
+}
 template <int S, typename MT>
 __device__ __forceinline__ int argmin_state(const MT (&M)[S], MT sentinel, MT& best) {
-  int idx = 0;
-  best = sentinel;
+  constexpr int W = (S + 31) / 32;
+  const MT mn = tree_min<S, MT>(M);
+  uint32_t ne[W];
 #pragma unroll
-  for (int s = 0; s < S; ++s) {
-    bool lt = M[s] < best;
-    best = lt ? M[s] : best;
-    idx = lt ? s : idx;
+  for (int w = 0; w < W; ++w) {
+    ne[w] = S < 32 ? ~0u : 0u;   // states past S differ
+    constexpr int top = S < 32 ? S : 32;
+#pragma unroll
+    for (int k = top - 1; k >= 0; --k)   // descending: state 32w + k ends up in bit k
+      ne[w] = __builtin_amdgcn_alignbit(ne[w], min_minus(mn, M[32 * w + k]), 31);
   }
-  return idx;
+  int idx;
+  if constexpr (W == 1) idx = __builtin_ctz(~ne[0]);
+  else idx = __builtin_ctzll(~(((uint64_t)ne[1] << 32) | ne[0]));
+  const bool found = mn < sentinel;   // nothing below the sentinel: state 0, best = sentinel
+  best = found ? mn : sentinel;
+  return found ? idx : 0;
 }
 
 // Walk decisions back from `st`, write the MSB-first output buffer, count errors.

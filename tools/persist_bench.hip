@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "acs_persist.hpp"
@@ -82,6 +83,73 @@ int trace(RegArgs a, int ngroups, int waves_per_cu, int cus, int n) {
   return 0;
 }
 
+// Interleaved A/B after a clock warm-up: each variant's sustained time in rounds A B C .. A B C ..,
+// so clock ramp and box-to-box power differences do not bias one variant.
+template <CodeSpec C, int AB, int BLEN = 40>
+float sustained(RegArgs a, int ngroups, int waves_per_cu, int cus, int n) {
+  auto kern = viterbi_soft_persist<C, BLEN, AB>;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0) != hipSuccess) return -1;
+  const int w = waves_per_cu < per_cu ? waves_per_cu : per_cu;
+  const int grid = w * cus < ngroups ? w * cus : ngroups;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  for (int rep = 0; rep < n; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, a, ngroups);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms / n;
+}
+
+// Paired A/B: production (A) against each variant (B) in ABBA blocks of 40 launches, so a linear
+// clock/thermal drift cancels; the ratio B/A per block quadruple, mean and spread over 4 quadruples.
+int ab(RegArgs a, int ng, int cus) {
+  sustained<kK7Ref, 0>(a, ng, 8, cus, 300);   // clock warm-up
+  RegArgs a42 = a;
+  a42.T = 48;
+  a42.blen = 42;
+  const int ng42 = (int)((size_t)a.nblocks * 46 / 48) / 64;
+  a42.nblocks = ng42 * 64;
+  const float scale42 = (float)((double)ng * 40 / ((double)ng42 * 42));   // per blen-40 bit
+  auto A = [&]() { return sustained<kK7Ref, 0>(a, ng, 8, cus, 40); };
+  struct V { const char* name; float (*f)(RegArgs, int, int, int, int); bool b42; };
+  const V vs[] = {
+    {"2-deep DMA", sustained<kK7Ref, kPersistDepth2>, false},
+    {"no DMA (stale LDS rows)", sustained<kK7Ref, kPersistNoDma>, false},
+    {"DMA, no LDS reads (synth)", sustained<kK7Ref, kPersistNoLdsRead>, false},
+    {"no memory, synth rows", sustained<kK7Ref, kPersistNoMem | kPersistNoMemRandom>, false},
+    {"line-aligned", sustained<kK7Ref, kPersistLineChunks>, false},
+    {"blen42 aligned (per bit)", sustained<kK7Ref, 0, 42>, true},
+    {"L2-resident input", sustained<kK7Ref, kPersistCachedInput>, false},
+    {"no traceback", sustained<kK7Ref, kPersistNoTraceback>, false},
+    {"no memory, int rows", sustained<kK7Ref, kPersistNoMem>, false},
+  };
+  double asum = 0;
+  int an = 0;
+  for (const V& v : vs) {
+    double r[4], rs = 0, lo = 1e9, hi = 0;
+    for (int q = 0; q < 4; ++q) {
+      auto B = [&]() { return v.b42 ? v.f(a42, ng42, 8, cus, 40) * scale42 : v.f(a, ng, 8, cus, 40); };
+      const float a0 = A(), b0 = B(), b1 = B(), a1 = A();
+      asum += a0 + a1;
+      an += 2;
+      r[q] = (b0 + b1) / (a0 + a1);
+      rs += r[q];
+      lo = r[q] < lo ? r[q] : lo;
+      hi = r[q] > hi ? r[q] : hi;
+    }
+    printf("%-26s time ratio vs production %.3f (%.3f .. %.3f)\n", v.name, rs / 4, lo, hi);
+  }
+  const double bits = (double)ng * 64 * 40;
+  printf("production mean %.4f ms  %.1f Gbit/s\n", asum / an, bits / (asum / an * 1e-3) / 1e9);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int nb = 1600000, T = 46;
   int cus = 0;
@@ -104,6 +172,7 @@ int main(int argc, char** argv) {
   a.blen = 40;
   a.out = d_out;
   const int ng = nb / 64;
+  if (argc > 1 && std::string(argv[1]) == "ab") return ab(a, ng, cus);
   if (argc > 1) {   // persist_bench trace [launches]
     const int n = argc > 2 ? atoi(argv[2]) : 300;
     trace<kK7Ref>(a, ng, 8, cus, n);
