@@ -495,7 +495,7 @@ __device__ __forceinline__ uint32_t lds_read_u8(uint32_t addr) {
   return r;
 }
 
-template <CodeSpec C, int BLEN>
+template <CodeSpec C, int BLEN, int MMODE = 2>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void viterbi_hard_persist(RegArgs a, int ngroups) {
   constexpr int S = 1 << (C.K - 1);
@@ -536,9 +536,15 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
     if (g + stride_groups < ngroups) issue_group(g + stride_groups, buf ^ 1);
     const uint32_t row_addr = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * kBuf + lane * T);
     const uint64_t info = load_info<BLEN>(a, b);
-    H16 M[S];
+    // metric type: 2 = plain uint16_t (production: v_add_u16 / v_min_u16, full rate, visible to the
+    // scheduler); 0 = H16 inline-asm ops (round 2 first cut: hipcc puts an s_nop 0 after every
+    // inline-asm VALU whose result is read next, 1,612 per group, 6 % slower); 1 = u32 (v_bcnt-folded
+    // adds and v_min_u32, half rate: 25 % slower). tools/persist_bench abh.
+    using MT = typename std::conditional<MMODE == 1, uint32_t,
+                                         typename std::conditional<MMODE >= 2, uint16_t, H16>::type>::type;
+    MT M[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) M[s].v = s ? 0xFF00u : 0u;   // viterbi-decoder.c:225-228
+    for (int s = 0; s < S; ++s) M[s] = MT{(MT)(s ? 0xFF00u : 0u)};   // viterbi-decoder.c:225-228
     DW D[BLEN];
     auto chunk_at = [&]<int c>() __attribute__((always_inline)) {
       if (c * PF >= a.T) return;   // always true: per-chunk basic blocks (see the soft kernel)
@@ -554,12 +560,16 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
         constexpr int t = c * PF + u;
         if constexpr (t < T) {
-          H16 BM[NS];
+          MT BM[NS];
 #pragma unroll
-          for (int k = 0; k < NS; ++k) BM[k].v = (uint32_t)__builtin_popcount((uint32_t)k ^ (sym[u] & kMask));
-          if constexpr (t < G) growth_step<C, t, H16>(M, BM, H16{0xFF00u});
+          for (int k = 0; k < NS; ++k) BM[k] = MT{(MT)__builtin_popcount((uint32_t)k ^ (sym[u] & kMask))};
+          if constexpr (MMODE == 2) {
+#pragma unroll
+            for (int k = 0; k < NS; ++k) asm volatile("" : "+v"(BM[k]));   // else hipcc folds the popcounts into every add (v_bcnt)
+          }
+          if constexpr (t < G) growth_step<C, t, MT>(M, BM, MT{(MT)0xFF00u});
           else {
-            D[t - G] = acs_step<C, false, H16>(M, BM);
+            D[t - G] = acs_step<C, false, MT>(M, BM);
             pin(D[t - G]);
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -575,7 +585,10 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
 
     uint32_t Mu[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) Mu[s] = M[s].v & 0xFFFFu;
+    for (int s = 0; s < S; ++s) {
+      if constexpr (MMODE >= 1) Mu[s] = M[s];
+      else Mu[s] = M[s].v & 0xFFFFu;
+    }
     uint32_t best;
     const uint32_t st = (uint32_t)argmin_state<S, uint32_t>(Mu, 0xFF00u, best);
     if (a.path_metric) a.path_metric[b] = (int32_t)best;

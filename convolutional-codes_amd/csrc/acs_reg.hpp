@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "trellis.hpp"
@@ -39,12 +40,15 @@ __device__ __forceinline__ float vmin(float a, float b) {
   return r;
 }
 __device__ __forceinline__ uint32_t vmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint16_t vmin(uint16_t a, uint16_t b) { return a < b ? a : b; }
 // 16-bit metrics (the BSC reference keeps uint16_t ones): v_add_u16 / v_min_u16 issue at full rate on
-// gfx950 where v_min_u32 is half rate (profiles/r01_rates_packed16.txt). H16 holds the metric in
-// the low half of a VGPR (high half don't-care); the ops are pinned by inline asm because hipcc
-// otherwise folds the branch-metric popcounts into every add (v_bcnt, half rate) and turns the
-// decision into compare + select. v_add_u16 / v_min_u16 zero the high half (measured: tools/t16), so
-// every metric stays zero-extended and the decision is the sign of the full-rate 32-bit m1 - m0.
+// gfx950 where v_min_u32 is half rate (profiles/r01_rates_packed16.txt). The hard kernels use plain
+// uint16_t: hipcc selects v_add_u16 / v_min_u16, knows they zero the high half, so the decision is
+// the sign of the full-rate 32-bit m1 - m0 with no extension; two things keep it there: the branch
+// metrics pass through an empty asm (else every add becomes a half-rate v_bcnt with accumulate) and
+// the decision words start from an opaque zero (acs_step). H16 below pins the same ops by inline asm
+// (the round-2 first cut, kept as the viterbi_hard_persist MMODE 0 ablation): hipcc cannot see into
+// the asm and puts an s_nop after every such op whose result is read next, 6 % slower.
 struct H16 {
   uint32_t v;
 };
@@ -67,6 +71,9 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t d, float m0, float m1) {
 __device__ __forceinline__ uint32_t shift_in(uint32_t d, uint32_t m0, uint32_t m1) {
   return (d << 1) | ((m1 - m0) >> 31);
 }
+__device__ __forceinline__ uint32_t shift_in(uint32_t d, uint16_t m0, uint16_t m1) {
+  return __builtin_amdgcn_alignbit(d, (uint32_t)m1 - (uint32_t)m0, 31);
+}
 __device__ __forceinline__ uint32_t shift_in(uint32_t d, H16 m0, H16 m1) {
   uint32_t diff;
   asm("v_sub_u32_e32 %0, %1, %2" : "=v"(diff) : "v"(m1.v), "v"(m0.v));
@@ -85,6 +92,10 @@ template <int HOLES>
 __device__ __forceinline__ uint32_t shift_in_n(uint32_t d, uint32_t m0, uint32_t m1) {
   if constexpr (HOLES == 0) return shift_in(d, m0, m1);
   else return __builtin_amdgcn_alignbit(d, m1 - m0, 31 - HOLES);
+}
+template <int HOLES>
+__device__ __forceinline__ uint32_t shift_in_n(uint32_t d, uint16_t m0, uint16_t m1) {
+  return __builtin_amdgcn_alignbit(d, (uint32_t)m1 - (uint32_t)m0, 31 - HOLES);
 }
 template <int HOLES>
 __device__ __forceinline__ uint32_t shift_in_n(uint32_t d, H16 m0, H16 m1) {
@@ -165,6 +176,12 @@ __device__ __forceinline__ DecWord<(1 << (C.K - 1))> acs_step(MT (&M)[1 << (C.K 
   constexpr int H = S / 2;
   MT N[S];
   uint32_t dlo = 0, dhi = 0;
+  if constexpr (std::is_same_v<MT, uint16_t> || std::is_same_v<MT, uint32_t>) {
+    // an opaque zero: alignbit(0, m1 - m0, 31) on integer metrics is otherwise folded into
+    // v_cmp -> VCC -> v_cndmask (~7 ns per instruction on gfx950, tools/raterbench6.hip)
+    asm volatile("" : "+v"(dlo));
+    asm volatile("" : "+v"(dhi));
+  }
   if constexpr (collapsed_mask<C>() == 0) {
 #pragma unroll
     for (int j = H - 1; j >= 0; --j) {
@@ -670,19 +687,21 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_hard_reg(RegArgs a) {
   }
   // afterwards every metric is <= n*T < 2^15: the ACS runs on 16-bit metrics, exactly the
   // reference's uint16_t arithmetic
-  H16 M16[S];
+  uint16_t M16[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) M16[s].v = M[s];
+  for (int s = 0; s < S; ++s) M16[s] = (uint16_t)M[s];
   pipelined_steps<kHardPF, uint32_t>(t0, T, [&](int t) { return (uint32_t)p[t]; },
                                      [&](uint32_t sym, int t) {
-                                       H16 BM[NS];
+                                       uint16_t BM[NS];
 #pragma unroll
-                                       for (int k = 0; k < NS; ++k)
-                                         BM[k].v = (uint32_t)__builtin_popcount((uint32_t)k ^ (sym & kMask));
-                                       dec[(size_t)t * dstride] = acs_step<C, false, H16>(M16, BM);
+                                       for (int k = 0; k < NS; ++k) {
+                                         BM[k] = (uint16_t)__builtin_popcount((uint32_t)k ^ (sym & kMask));
+                                         asm volatile("" : "+v"(BM[k]));   // no v_bcnt-folded adds
+                                       }
+                                       dec[(size_t)t * dstride] = acs_step<C, false, uint16_t>(M16, BM);
                                      });
 #pragma unroll
-  for (int s = 0; s < S; ++s) M[s] = M16[s].v & 0xFFFFu;
+  for (int s = 0; s < S; ++s) M[s] = M16[s];
   uint32_t errors = 0;
   if (b < nb) {
     uint32_t best;

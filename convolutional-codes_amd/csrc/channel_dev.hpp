@@ -267,24 +267,27 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
     }
   };
   // BSC saturation (reference :127-130) only matters while states are unreachable (t < K-1);
-  // afterwards the hard ACS runs on 16-bit metrics (H16, acs_reg.hpp), like viterbi_hard_reg
+  // afterwards the hard ACS runs on 16-bit metrics (uint16_t), like viterbi_hard_reg
   const int t0 = HARD ? (T < C.K - 1 ? T : C.K - 1) : 0;
   if constexpr (HARD) {
     run(std::true_type{}, 0, t0);
-    H16 M16[S];
+    uint16_t M16[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) M16[s].v = M[s];
+    for (int s = 0; s < S; ++s) M16[s] = (uint16_t)M[s];
 #pragma unroll 1
     for (int t = t0; t < T; ++t) {
       MT BM[NS];
       src.next(BM);
-      H16 B16[NS];
+      uint16_t B16[NS];
 #pragma unroll
-      for (int k = 0; k < NS; ++k) B16[k].v = BM[k];
-      dec[(size_t)t * dstride] = acs_step<C, false, H16>(M16, B16);
+      for (int k = 0; k < NS; ++k) {
+        B16[k] = (uint16_t)BM[k];
+        asm volatile("" : "+v"(B16[k]));   // no v_bcnt-folded adds
+      }
+      dec[(size_t)t * dstride] = acs_step<C, false, uint16_t>(M16, B16);
     }
 #pragma unroll
-    for (int s = 0; s < S; ++s) M[s] = M16[s].v & 0xFFFFu;
+    for (int s = 0; s < S; ++s) M[s] = M16[s];
   } else {
     run(std::false_type{}, t0, T);
   }

@@ -150,6 +150,61 @@ int ab(RegArgs a, int ng, int cus) {
   return 0;
 }
 
+template <CodeSpec C, int MM>
+float sustained_hard(RegArgs a, int ngroups, int waves_per_cu, int cus, int n) {
+  auto kern = viterbi_hard_persist<C, 40, MM>;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0) != hipSuccess) return -1;
+  const int w = waves_per_cu < per_cu ? waves_per_cu : per_cu;
+  const int grid = w * cus < ngroups ? w * cus : ngroups;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  for (int rep = 0; rep < n; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, a, ngroups);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms / n;
+}
+
+// BSC persistent kernel: 16-bit inline-asm metrics (production) against plain u32 metrics, ABBA.
+template <int MODE>
+int ab_hard(int cus) {
+  const int nb = 1600000, T = 46, ng = nb / 64;
+  std::vector<uint8_t> h((size_t)nb * T);
+  uint32_t x = 777;
+  for (auto& v : h) {
+    x = x * 1664525u + 1013904223u;
+    v = (uint8_t)(x >> 30);
+  }
+  uint8_t *d_in, *d_out;
+  CHECK(hipMalloc(&d_in, h.size()));
+  CHECK(hipMalloc(&d_out, (size_t)nb * 8));
+  CHECK(hipMemcpy(d_in, h.data(), h.size(), hipMemcpyHostToDevice));
+  RegArgs a{};
+  a.in = d_in;
+  a.T = T;
+  a.nblocks = nb;
+  a.blen = 40;
+  a.out = d_out;
+  sustained_hard<kK7Ref, 0>(a, ng, 8, cus, 300);
+  double rs = 0, asum = 0;
+  for (int q = 0; q < 4; ++q) {
+    const float a0 = sustained_hard<kK7Ref, 0>(a, ng, 8, cus, 40), b0 = sustained_hard<kK7Ref, MODE>(a, ng, 8, cus, 40),
+                b1 = sustained_hard<kK7Ref, MODE>(a, ng, 8, cus, 40), a1 = sustained_hard<kK7Ref, 0>(a, ng, 8, cus, 40);
+    rs += (b0 + b1) / (a0 + a1);
+    asum += a0 + a1;
+    printf("quad %d: h16 %.4f %.4f  u32 %.4f %.4f\n", q, a0, a1, b0, b1);
+  }
+  printf("hard mode %d metrics: time ratio vs h16", MODE); printf(" %.3f; h16 %.4f ms %.1f Gbit/s\n", rs / 4, asum / 8,
+         (double)ng * 64 * 40 / (asum / 8 * 1e-3) / 1e9);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int nb = 1600000, T = 46;
   int cus = 0;
@@ -173,6 +228,7 @@ int main(int argc, char** argv) {
   a.out = d_out;
   const int ng = nb / 64;
   if (argc > 1 && std::string(argv[1]) == "ab") return ab(a, ng, cus);
+  if (argc > 1 && std::string(argv[1]) == "abh") return ab_hard<1>(cus) | ab_hard<2>(cus);
   if (argc > 1) {   // persist_bench trace [launches]
     const int n = argc > 2 ? atoi(argv[2]) : 300;
     trace<kK7Ref>(a, ng, 8, cus, n);
