@@ -50,8 +50,10 @@ struct Philox {
     uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = 0x43435631u, y0 = k0, y1 = k1;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-      const uint32_t h0 = __umulhi(0xD2511F53u, x0), l0 = 0xD2511F53u * x0;
-      const uint32_t h1 = __umulhi(0xCD9E8D57u, x2), l1 = 0xCD9E8D57u * x2;
+      // one v_mad_u64_u32 per product (hi and lo together) instead of v_mul_hi + v_mul_lo
+      const uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+      const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+      const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
       x0 = h1 ^ x1 ^ y0; x1 = l1;
       x2 = h0 ^ x3 ^ y1; x3 = l0;
       y0 += 0x9E3779B9u; y1 += 0xBB67AE85u;
@@ -69,6 +71,30 @@ struct Philox {
     return r >> 1;
   }
 };
+
+// Division by the channel's two constants in three instructions instead of the IEEE sequence
+// (v_div_scale / v_div_fmas / v_div_fixup, ~10): Markstein's correction q0 = a*r, e = fma(-q0, b, a)
+// (exact), q = fma(e, r, q0) with r = RN(1/b). Checked bit-identical to IEEE division, on the device,
+// for EVERY operand of the domain (tools/divcheck.hip, profiles/r02_divcheck.txt):
+//  * k / 2147483647.0 for all k < 2^31 (gaussian.c:23-24: the uniform draws);
+//  * x / ndist for all 2^-60 <= x < 2^64, for the ndist of the n = 1, 2, 3 constellations
+//    (demapper.c:70). The squared distances stay in that range: a nonzero |x - p| is at least half an
+//    ulp of a constellation coordinate (>= 2^-25), and |noise| <= 6.56 * scaling (Box-Muller of a
+//    31-bit uniform), so the host requires scaling < 2^28 (ccv_simulate_device) -- Eb/N0 > -160 dB.
+__device__ __forceinline__ double div_rand_max(uint32_t k) {
+  constexpr double M = 2147483647.0, R = 1.0 / M;
+  const double a = (double)k;
+  const double q0 = a * R;
+  const double e = __builtin_fma(-q0, M, a);
+  return __builtin_fma(e, R, q0);
+}
+template <float B>
+__device__ __forceinline__ float div_const(float a) {
+  constexpr float R = 1.0f / B;
+  const float q0 = a * R;
+  const float e = __builtin_fmaf(-q0, B, a);
+  return __builtin_fmaf(e, R, q0);
+}
 
 // common/constellations.c:6-28 (index = symbol value).
 template <int N>
@@ -197,8 +223,8 @@ struct ChannelSource {
       }
       double u1, u2;
       do {
-        u1 = (double)rng.next() / 2147483647.0;
-        u2 = (double)rng.next() / 2147483647.0;
+        u1 = div_rand_max(rng.next());
+        u2 = div_rand_max(rng.next());
       } while (u1 == 0.0);
       const double R = sqrt(-2.0 * log(u1));
       const double Tt = 2.0 * 3.14159265358979323846 * u2;   // 2.0 * M_PI * u2
@@ -226,7 +252,7 @@ struct ChannelSource {
 #pragma unroll
       for (int k = 0; k < NS; ++k) {
         const float dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
-        BM[k] = ((dx * dx) + (dy * dy)) / nd;
+        BM[k] = div_const<nd>((dx * dx) + (dy * dy));
       }
       if (out && t < T) {
         float* o = reinterpret_cast<float*>(out) + (size_t)t * NS;

@@ -598,6 +598,10 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   const bool hard = p->d.channel == CCV_HARD;
   if (hard && !(channel_param >= 0.0 && channel_param <= 1000000.0))
     return fail("BSC p_ppm must be in [0, 1e6]");
+  // the demapper's 3-instruction division is exact for squared distances below 2^64, which holds
+  // for noise scalings below 2^28 (channel_dev.hpp div_const; Eb/N0 above -160 dB)
+  if (!hard && !(channel_param >= 0.0 && channel_param < 268435456.0))
+    return fail("AWGN noise scaling must be in [0, 2^28)");
   hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
   if (!d_info) {
     if (p->sim_info.grow(nblocks * (size_t)p->d.info_bytes, stream)) return -1;

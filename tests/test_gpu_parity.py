@@ -278,6 +278,11 @@ def test_dropped_plans_release_device_memory(torch_cuda):
     does not leak device memory (nor streams)."""
     import gc
     torch = torch_cuda
+    # the first plans of a process load the code objects and the runtime's own pools (~150 MB when
+    # this test runs first): one create/reserve/drop of each kind before the baseline
+    for ch_ in (SOFT, HARD):
+        with Plan(K7, ch_, FLAG_GLOBAL_DECISIONS) as plan:
+            plan.reserve(1_600_000)
     torch.cuda.synchronize()
     gc.collect()
     free0, _ = torch.cuda.mem_get_info()
