@@ -20,6 +20,7 @@
 #include <type_traits>
 
 #include "acs_multi.hpp"
+#include "acs_persist.hpp"
 #include "acs_reg.hpp"
 #include "trellis.hpp"
 
@@ -34,6 +35,7 @@ struct ChanArgs {
   int hard_demap;            // AWGN: common/hard-demapper.c instead of common/demapper.c
   uint8_t* info_out;         // [nb][IB] transmitted info bytes (required)
   void* ch_out;              // optional export: soft float [nb][T][2^n] / hard uint8 [nb][T]
+  int global_decisions;      // K <= 7: decisions through r.dec in HBM instead of LDS (A/B, long T)
 };
 
 // Philox4x32-10 with one counter stream per block (key = seed, counter = (block, draw, 0, tag)).
@@ -326,6 +328,102 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
     }
     errors = traceback<C.K>(a.r, b, st);
   }
+  accumulate_errors(a.r, errors);
+}
+
+// K <= 7 with the survivor decisions in LDS instead of HBM: the main steps' words go to
+// lds[t - G][lane] (20 KiB per wave at K=7, blen 40: two waves per SIMD, the VGPR budget's
+// occupancy anyway), the first K-1 steps are growth steps (acs_persist.hpp growth_step: one add per
+// reachable state, decision 0, nothing stored), and the traceback reads the lane's column back with
+// the history word of traceback_regs -- no decision traffic to HBM (2 x 8 B per step per block).
+// The output bit of step t is bit t of H = (st << F) | sum d_m 2^m (F = T - (K-1) main steps, d_m the
+// decision read at main step m): byte k is bit-reversed bits 8k .. 8k+7, emitted as the walk passes.
+template <int K, typename DW>
+__device__ __forceinline__ uint32_t traceback_lds(const RegArgs& a, const DW* col, int b, uint32_t st,
+                                                  bool owner) {
+  constexpr uint32_t S = 1u << (K - 1);
+  const int T = a.T, F = T - (K - 1), OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+  uint8_t* out = a.out + (size_t)b * OB;
+  const uint8_t* info = a.info != nullptr ? a.info + (size_t)b * IB : nullptr;
+  uint32_t errors = 0;
+  auto emit = [&](int k, uint32_t bits8) {   // bits8: bit j = output of step 8k + j
+    const uint32_t byte = __builtin_bitreverse32(bits8) >> 24;
+    if (owner) out[k] = (uint8_t)byte;
+    if (info != nullptr && k < IB) {
+      const int valid = a.blen - 8 * k;
+      const uint32_t mask = valid >= 8 ? 0xFFu : (0xFFu << (8 - valid)) & 0xFFu;
+      errors += __builtin_popcount((byte ^ info[k]) & mask);
+    }
+  };
+  // bytes made of final-state bits only
+  for (int k = OB - 1; 8 * k >= F; --k) emit(k, (st >> (8 * k - F)) & 0xFFu);
+  uint32_t h = st;
+#pragma unroll 8
+  for (int m = F - 1; m >= 0; --m) {
+    const uint32_t d = (uint32_t)(col[(size_t)m * kRegThreads] >> (h & (S - 1)));
+    h = (h << 1) | (d & 1u);
+    if ((m & 7) == 0) emit(m >> 3, h & 0xFFu);
+  }
+  return owner ? errors : 0u;
+}
+
+template <CodeSpec C, bool HARD>
+__global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
+  constexpr int S = 1 << (C.K - 1);
+  constexpr int NS = 1 << C.n;
+  constexpr int G = C.K - 1;
+  using DW = DecWord<S>;
+  using Src = ChannelSource<C, HARD>;
+  using SM = typename Src::MT;                                      // source metric type
+  using MT = typename std::conditional<HARD, uint16_t, float>::type;   // ACS metric type
+  extern __shared__ __attribute__((aligned(16))) unsigned char chan_lds[];
+  DW* dl = reinterpret_cast<DW*>(chan_lds);
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x * kRegThreads + lane;
+  const int T = a.r.T, nb = a.r.nblocks;
+  const int bc = b < nb ? b : nb - 1;
+  Src src;
+  src.init(a, bc, b < nb);
+  MT M[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if constexpr (HARD) M[s] = (MT)(s ? 0xFF00u : 0u);   // viterbi-decoder.c:225-228
+    else M[s] = s ? __builtin_inff() : 0.0f;           // viterbi-decoder.c:212-218
+  }
+  auto next_bm = [&](MT (&BM)[NS]) __attribute__((always_inline)) {
+    SM raw[NS];
+    src.next(raw);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      BM[k] = (MT)raw[k];
+      if constexpr (HARD) asm volatile("" : "+v"(BM[k]));   // no v_bcnt-folded adds (acs_reg.hpp)
+    }
+  };
+  // T >= K > G: every block has its K-1 growth steps
+  [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
+    ([&]() __attribute__((always_inline)) {
+      MT BM[NS];
+      next_bm(BM);
+      growth_step<C, ts, MT>(M, BM, HARD ? (MT)0xFF00u : (MT)__builtin_inff());
+    }(), ...);
+  }(std::make_integer_sequence<int, G>{});
+#pragma unroll 1
+  for (int t = G; t < T; ++t) {
+    MT BM[NS];
+    next_bm(BM);
+    dl[(size_t)(t - G) * kRegThreads + lane] = acs_step<C, false, MT>(M, BM);
+  }
+  // each lane reads back only its own column: no barrier
+  using AM = typename std::conditional<HARD, uint32_t, float>::type;
+  AM Ma[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) Ma[s] = (AM)M[s];
+  AM best;
+  const uint32_t st = (uint32_t)argmin_state<S, AM>(Ma, HARD ? (AM)0xFF00u : (AM)__builtin_inff(), best);
+  if constexpr (HARD) {
+    if (b < nb && a.r.path_metric) a.r.path_metric[b] = (int32_t)best;
+  }
+  const uint32_t errors = traceback_lds<C.K, DW>(a.r, dl + lane, bc, st, b < nb);
   accumulate_errors(a.r, errors);
 }
 

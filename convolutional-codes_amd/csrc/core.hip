@@ -631,6 +631,7 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   if (hard && a.hard_demap) return fail("the hard demapper belongs to the AWGN channel");
   a.info_out = d_info;
   a.ch_out = d_channel;
+  a.global_decisions = p->global_decisions ? 1 : 0;
   const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
   const bool multi = p->reg_index < 0;
   HIP_TRY(ccv::channel_launchers(multi, hard)[multi ? p->multi_index : p->reg_index](a, grid, stream));

@@ -10,10 +10,18 @@
 namespace ccv {
 namespace {
 
+// LDS budget of the decision column array per wave: 20 KiB keeps two waves per SIMD (160 KiB per CU)
+constexpr size_t kChanLdsBudget = 20 * 1024;
+
 template <size_t I, bool HARD>
 hipError_t launch_reg(const ChanArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((viterbi_channel_reg<kRegCodes[I], HARD>), dim3(grid), dim3(kRegThreads), 0,
-                     stream, a);
+  constexpr CodeSpec C = kRegCodes[I];
+  constexpr size_t word = (1u << (C.K - 1)) > 32 ? 8 : 4;
+  const size_t lds = (size_t)(a.r.T - (C.K - 1)) * word * kRegThreads;
+  if (!a.global_decisions && lds <= kChanLdsBudget)
+    hipLaunchKernelGGL((viterbi_channel_lds<C, HARD>), dim3(grid), dim3(kRegThreads), lds, stream, a);
+  else
+    hipLaunchKernelGGL((viterbi_channel_reg<C, HARD>), dim3(grid), dim3(kRegThreads), 0, stream, a);
   return hipGetLastError();
 }
 
