@@ -331,11 +331,13 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
   accumulate_errors(a.r, errors);
 }
 
-// K <= 7 with the survivor decisions in LDS instead of HBM: the main steps' words go to
-// lds[t - G][lane] (20 KiB per wave at K=7, blen 40: two waves per SIMD, the VGPR budget's
-// occupancy anyway), the first K-1 steps are growth steps (acs_persist.hpp growth_step: one add per
-// reachable state, decision 0, nothing stored), and the traceback reads the lane's column back with
-// the history word of traceback_regs -- no decision traffic to HBM (2 x 8 B per step per block).
+// K <= 7 with the survivor decisions in LDS instead of HBM (the BSC default, core.hip):
+// the main steps' words go to lds[t - G][lane] (20 KiB per wave at K=7, blen 40), the first K-1
+// steps are growth steps (acs_persist.hpp growth_step: one add per reachable state, decision 0,
+// nothing stored), and the traceback reads the lane's column back with the history word of
+// traceback_regs -- no decision traffic to HBM (2 x 8 B per step per block). The column caps a CU at
+// 8 waves: BSC gains (108.6 vs 96.6 Gbit/s, K=7), the double-precision AWGN channel, whose
+// viterbi_channel_reg runs 12 waves per CU, loses (60.3 vs 62.5).
 // The output bit of step t is bit t of H = (st << F) | sum d_m 2^m (F = T - (K-1) main steps, d_m the
 // decision read at main step m): byte k is bit-reversed bits 8k .. 8k+7, emitted as the walk passes.
 template <int K, typename DW>

@@ -631,7 +631,13 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   if (hard && a.hard_demap) return fail("the hard demapper belongs to the AWGN channel");
   a.info_out = d_info;
   a.ch_out = d_channel;
-  a.global_decisions = p->global_decisions ? 1 : 0;
+  // Decisions in LDS (viterbi_channel_lds) for BSC, in HBM scratch for AWGN: the 20 KiB column per
+  // wave caps a CU at 8 waves; the BSC kernel gains more from the saved decision traffic (108.6 vs
+  // 96.6 Gbit/s at K=7), the double-precision AWGN kernel loses more occupancy than it saves (60.3
+  // vs 62.5). CCV_CHANNEL_LDS_DECISIONS=1 / =0 forces either (A/B).
+  const char* lds_env = std::getenv("CCV_CHANNEL_LDS_DECISIONS");
+  const bool lds_dec = lds_env && lds_env[0] ? lds_env[0] == '1' : hard;
+  a.global_decisions = (p->global_decisions || !lds_dec) ? 1 : 0;
   const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
   const bool multi = p->reg_index < 0;
   HIP_TRY(ccv::channel_launchers(multi, hard)[multi ? p->multi_index : p->reg_index](a, grid, stream));

@@ -10,7 +10,7 @@
 namespace ccv {
 namespace {
 
-// LDS budget of the decision column array per wave: 20 KiB keeps two waves per SIMD (160 KiB per CU)
+// LDS budget of the decision column array per wave (opt-in kernel): 20 KiB = 8 waves per CU
 constexpr size_t kChanLdsBudget = 20 * 1024;
 
 template <size_t I, bool HARD>

@@ -570,8 +570,8 @@ def _simulate(torch, plan, c, seed, first, nb, param, hard_demap=False):
 CHANNEL_CODES = [("k7", K7), ("k7_true", K7.with_(gen_mode=GEN_TRUE_PARITY)), ("code0", CODEBOOK[0]),
                  ("code5_r13", CODEBOOK[5]), ("k8", K8), ("k9_true", K9.with_(gen_mode=GEN_TRUE_PARITY)),
                  ("k9_blen255", K9.with_(blen=255)), ("k7_blen1", K7.with_(blen=1)),
-                 # K <= 7 keep the decisions in LDS while the column fits 20 KiB per wave: code3
-                 # (K=6) at blen 80 just fits, K=7 at blen 100 takes the HBM-scratch kernel
+                 # longer blocks (and the LDS-decision kernel's limit: code3 = K=6 at blen 80 fits
+                 # its 20 KiB column, K=7 at blen 100 does not)
                  ("code3_blen80", CODEBOOK[3].with_(blen=80)), ("k7_blen100", K7.with_(blen=100))]
 
 
@@ -637,12 +637,20 @@ def test_device_channel_ber_sweep_matches_host(torch_cuda):
 
 @pytest.mark.parametrize("channel", [SOFT, HARD])
 def test_device_channel_lds_vs_hbm_decisions(torch_cuda, channel):
-    """The LDS-decision channel kernel and the HBM-scratch one (CCV_FLAG_GLOBAL_DECISIONS) decode the
-    same device-generated frames identically (outputs, path metrics, error counts)."""
+    """The LDS-decision channel kernel (CCV_CHANNEL_LDS_DECISIONS=1, the BSC default) and the
+    HBM-scratch one (=0, the AWGN default) decode the same device-generated frames identically
+    (outputs, path metrics, error counts)."""
+    import os
     param = 70000 if channel == HARD else ch.noise_scaling(1.0)
-    for c in (K7, CODEBOOK[0]):
-        a = _simulate(torch_cuda, Plan(c, channel), c, 3, 5000, 777, param)
-        b = _simulate(torch_cuda, Plan(c, channel, FLAG_GLOBAL_DECISIONS), c, 3, 5000, 777, param)
+    for c in (K7, CODEBOOK[0], CODEBOOK[3].with_(blen=80), K7.with_(blen=1)):
+        runs = []
+        for forced in ("1", "0"):
+            os.environ["CCV_CHANNEL_LDS_DECISIONS"] = forced
+            try:
+                runs.append(_simulate(torch_cuda, Plan(c, channel), c, 3, 5000, 777, param))
+            finally:
+                del os.environ["CCV_CHANNEL_LDS_DECISIONS"]
+        a, b = runs
         for x, y in zip(a[:4], b[:4]):
             if channel == SOFT and x is a[3]:
                 continue   # path metrics are hard-decision only
