@@ -18,6 +18,7 @@
 
 namespace ccv {
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s);   // stack.hip
+bool stack_rows_eligible(int n, int K, int T);                           // stack.hip
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s);     // stack.hip
 }
 
@@ -578,7 +579,13 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
   a.info = d_info;
   a.err = d_info ? d_errors : nullptr;
   a.status = d_status;
-  HIP_TRY(ccv::launch_stack(a, p->d.channel == CCV_HARD, reinterpret_cast<hipStream_t>(stream_v)));
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+  if (ccv::stack_rows_eligible(a.n, a.K, a.T)) {   // persistent rows pull blocks from a counter
+    if (p->counter.grow(sizeof(unsigned int), stream)) return -1;
+    HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, sizeof(unsigned int), stream));
+    a.next_block = static_cast<unsigned int*>(p->counter.ptr);
+  }
+  HIP_TRY(ccv::launch_stack(a, p->d.channel == CCV_HARD, stream));
   return 0;
 }
 

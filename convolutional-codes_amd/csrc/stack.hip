@@ -25,7 +25,37 @@ static hipError_t launch_pw(const StackArgs& a, size_t lds, hipStream_t s) {
   return launch_v<HARD, PW, 0, false>(a, lds, s);
 }
 
+// Four searches per wave (stack_decode_rows) as persistent rows: as many waves as the chip holds
+// at once, capped by the blocks (4 per wave).
+template <bool HARD, int NP>
+static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
+  const void* fn = reinterpret_cast<const void*>(&stack_decode_rows<HARD, NP>);
+  const size_t lds = (size_t)kStackRows * stack_rows_row_bytes(a.T, HARD ? 1 : 1 << NP, HARD);
+  int dev = 0, cus = 0, per_cu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kStackDepth, lds);
+  if (e != hipSuccess) return e;
+  const long resident = (long)(cus > 0 ? cus : 1) * (per_cu > 0 ? per_cu : 1);
+  const long waves_needed = ((long)a.nblocks + kStackRows - 1) / kStackRows;
+  const int grid = (int)(waves_needed < resident ? waves_needed : resident);
+  if (std::getenv("CCV_STACK_DEBUG"))
+    std::fprintf(stderr, "stack rows: lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n", lds, per_cu, cus, grid);
+  hipLaunchKernelGGL((stack_decode_rows<HARD, NP>), dim3(grid), dim3(kStackDepth), lds, s, a);
+  return hipGetLastError();
+}
+
+bool stack_rows_eligible(int n, int K, int T) {
+  if (const char* env = std::getenv("CCV_STACK_WAVE"))   // A/B: one search per wave
+    if (env[0] == '1') return false;
+  return K <= 32 && (n == 2 || n == 3) && T <= kRowsMaxT;
+}
+
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
+  if (stack_rows_eligible(a.n, a.K, a.T) && a.next_block != nullptr) {
+    if (hard) return a.n == 2 ? launch_rows<true, 2>(a, s) : launch_rows<true, 3>(a, s);
+    return a.n == 2 ? launch_rows<false, 2>(a, s) : launch_rows<false, 3>(a, s);
+  }
   const size_t per = (size_t)a.T * (hard ? 1 : ((size_t)1 << a.n));
   const size_t lds = 2 * per * (hard ? 1 : sizeof(float));
   const int pw = (a.T + 31) / 32;

@@ -46,6 +46,7 @@ struct StackArgs {
   const uint8_t* info;     // optional [nb][IB]: count bit errors
   unsigned long long* err;
   int32_t* status;         // optional [nb]: 0 ok, 1 = the reference would read past its buffers
+  unsigned int* next_block;  // stack_decode_rows: work counter, zero before the launch
 };
 
 constexpr int kStackDepth = 64;   // stack-decoder.c:12 == wave64
@@ -257,6 +258,232 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode(StackArgs a) {
     if (lane == 0 && a.path_metric) a.path_metric[b] = bcast(met, status ? 0 : cur);
   }
   if (lane == 0 && a.status) a.status[b] = status;
+  if (a.err) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) errors += __shfl_xor(errors, off, 64);
+    if (lane == 0 && errors) atomicAdd(a.err, (unsigned long long)errors);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Four searches per wave (round 2). The one-search-per-wave kernel above is bound by the CU's one
+// scalar unit: every search iteration is ~50 SALU plus the branches of its wave-uniform control
+// flow (profiles/r01_pmc_stack.txt: ~78 CU cycles per iteration). Here each 16-lane DPP row runs
+// its own search and keeps a whole 64-entry stack, entry e in lane e % 16, slot e / 16, so:
+//   * the scans are row reductions (quad_perm, row_half_mirror, row_mirror: every lane of the row
+//     ends with the result, no readlane) -- max / min, then the lowest index among the equal ones
+//     as a second u32 min reduction over per-lane candidates;
+//   * all bookkeeping (frontier t, stack size, status) is row-uniform VALU state, so the four
+//     searches share one instruction stream and the scalar unit only runs the loop;
+//   * metrics stay in VGPRs (4 slots per lane, for the scans); the rest of an entry -- next index
+//     and expected symbols packed, 32-bit encoder state, 64 path bits -- is one 16-byte LDS record
+//     per entry, so the current path's record is one broadcast ds_read_b128 and an update one
+//     ds_write_b128 by the row's lane 0 (current path) and lane 1 (duplicate);
+//   * rows are persistent: a row that finishes its block writes the output and takes the next
+//     block from a global counter, so a long search holds up only its own row.
+// Same arithmetic, tie rules and streaming quirks as stack_decode (the previous block's symbols
+// are read from global memory when a path runs ahead of the frontier). K <= 32 (32-bit state),
+// n = NP in {2, 3}, T <= 64 (two path words); other codes use stack_decode.
+constexpr int kStackRows = 4;                        // searches per wave
+constexpr int kRowLanes = kStackDepth / kStackRows;  // 16: one DPP row
+constexpr int kRowSlots = kStackDepth / kRowLanes;   // 4 stack entries per lane
+constexpr int kRowsMaxT = 64;
+
+// row-wide reductions (every lane of the 16-lane row gets the result); explicit s_nop for the
+// VALU-write -> DPP-read hazard, as CCV_WAVE_REDUCE
+#define CCV_ROW_STEP(op, ctrl) "s_nop 1\n" op "_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf\n"
+#define CCV_ROW_REDUCE(op)                                                                     \
+  CCV_ROW_STEP(op, "quad_perm:[1,0,3,2]") CCV_ROW_STEP(op, "quad_perm:[2,3,0,1]")             \
+  CCV_ROW_STEP(op, "row_half_mirror") CCV_ROW_STEP(op, "row_mirror")
+__device__ __forceinline__ float row_max(float v) { asm volatile(CCV_ROW_REDUCE("v_max_f32") : "+v"(v)); return v; }
+__device__ __forceinline__ float row_min(float v) { asm volatile(CCV_ROW_REDUCE("v_min_f32") : "+v"(v)); return v; }
+__device__ __forceinline__ int32_t row_max(int32_t v) { asm volatile(CCV_ROW_REDUCE("v_max_i32") : "+v"(v)); return v; }
+__device__ __forceinline__ int32_t row_min(int32_t v) { asm volatile(CCV_ROW_REDUCE("v_min_i32") : "+v"(v)); return v; }
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) { asm volatile(CCV_ROW_REDUCE("v_min_u32") : "+v"(v)); return v; }
+#undef CCV_ROW_REDUCE
+#undef CCV_ROW_STEP
+
+__device__ __forceinline__ float vmax2(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ int32_t vmax2(int32_t a, int32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ float vmin2(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ int32_t vmin2(int32_t a, int32_t b) { return a < b ? a : b; }
+
+// LDS bytes per row: the block's symbols (16-byte aligned), then 65 entry records (64 + a dummy)
+__host__ __device__ constexpr size_t stack_rows_sym_bytes(int T, int ns, bool hard) {
+  return (((size_t)T * (size_t)ns * (hard ? 1 : 4)) + 15) & ~(size_t)15;
+}
+__host__ __device__ constexpr size_t stack_rows_row_bytes(int T, int ns, bool hard) {
+  return stack_rows_sym_bytes(T, ns, hard) + (size_t)(kStackDepth + 1) * 16;
+}
+
+template <bool HARD, int NP>
+__global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
+  using MT = typename std::conditional<HARD, int32_t, float>::type;
+  using ET = typename std::conditional<HARD, uint8_t, float>::type;
+  constexpr int NS = HARD ? 1 : (1 << NP);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int l = lane & (kRowLanes - 1);
+  const int rbase = lane & ~(kRowLanes - 1);
+  const int T = a.T, K = a.K, nb = a.nblocks;
+  const int per = T * NS;
+  const size_t sym_bytes = stack_rows_sym_bytes(T, NS, HARD);
+  unsigned char* rowp = smem + (size_t)(lane / kRowLanes) * stack_rows_row_bytes(T, NS, HARD);
+  ET* syms = reinterpret_cast<ET*>(rowp);
+  uint4* ent = reinterpret_cast<uint4*>(rowp + sym_bytes);   // [65] records
+  const ET* in = reinterpret_cast<const ET*>(a.in);
+  const ET* prev_caller = reinterpret_cast<const ET*>(a.prev);
+  uint64_t poly[kMaxN];
+#pragma unroll
+  for (int k = 0; k < kMaxN; ++k) poly[k] = a.poly[k];
+  const bool idiom = a.gen == GEN_REF_X86;
+  const uint32_t symmask = (1u << NP) - 1u;
+  const MT lo_sent = HARD ? (MT)INT32_MIN : (MT)-__builtin_inff();
+  const MT hi_sent = HARD ? (MT)INT32_MAX : (MT)__builtin_inff();
+  const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
+  // record: x = next index | expected symbols (e0 << 8 | e1) << 8, y = encoder state, z/w = path
+  auto symbols_of = [&](uint32_t st) { return lane_symbols<NP, true>(poly, NP, K, idiom, (uint64_t)st); };
+  const uint32_t esym_root = symbols_of(0);
+
+  auto fetch = [&]() -> int {
+    uint32_t b = 0;
+    if (l == 0) b = atomicAdd(a.next_block, 1u);
+    return __shfl((int)b, rbase, 64);
+  };
+  // stage a block's symbols and the root entry; the row's LDS is private to its 16 lanes
+  auto stage = [&](int b) {
+    const ET* src = in + (size_t)b * per;
+    for (int i = l; i < per; i += kRowLanes) {
+      ET v = src[i];
+      if constexpr (HARD) v = (ET)(v & symmask);   // binary-symmetric-channel/stack-decoder.c:116-118
+      syms[i] = v;
+    }
+    if (l == 0) ent[0] = make_uint4(esym_root << 8, 0u, 0u, 0u);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  };
+
+  MT met[kRowSlots];   // entry k * 16 + l; entries not on the stack hold the low sentinel
+#pragma unroll
+  for (int k = 0; k < kRowSlots; ++k) met[k] = (k == 0 && l == 0) ? (MT)0 : lo_sent;
+  int blk = fetch();
+  bool live_row = blk < nb;
+  int t = 1, size = 1, status = 0;
+  if (live_row) stage(blk);
+  uint32_t errors = 0;
+
+  while (__ballot(live_row) != 0) {
+    if (live_row) {
+      // get_most_probable_path (stack-decoder.c:213-225): strict > from -inf, first index wins.
+      // Entries not yet on the stack hold -inf / INT32_MIN (never a hit), so the scan needs no
+      // liveness test; the least-probable scan below only matters once all 64 are live.
+      const MT mx = row_max(vmax2(vmax2(met[0], met[1]), vmax2(met[2], met[3])));
+      uint32_t cand = kStackDepth;
+#pragma unroll
+      for (int k = kRowSlots - 1; k >= 0; --k) cand = met[k] == mx ? (uint32_t)(k * kRowLanes + l) : cand;
+      const uint32_t cur = row_min_u32(cand);
+      const bool ok = mx > lo_sent;
+      // the common path is branch-free: every quantity is computed, the outcome selected
+      const uint4 rec = ent[ok ? cur : (uint32_t)kStackDepth];
+      const uint32_t c_next = rec.x & 0xFFu;
+      const bool adv = ok && c_next == (uint32_t)t;          // the path ends at the frontier
+      bool bad = !ok || (!adv && c_next >= (uint32_t)T);     // would read past the input buffer
+      bool ext = !adv && !bad;
+      const uint32_t e0 = (rec.x >> 16) & 0xFFu, e1 = (rec.x >> 8) & 0xFFu;
+      const uint32_t ci = c_next < (uint32_t)T ? c_next : (uint32_t)T - 1u;
+      ET r0, r1;
+      if constexpr (HARD) { r0 = r1 = syms[ci]; }
+      else { r0 = syms[ci * NS + e0]; r1 = syms[ci * NS + e1]; }
+      if (ext && c_next >= (uint32_t)t) {
+        // symbols at or beyond the frontier are still the previous block's (header of stack_decode)
+        const ET* pv = blk > 0 ? in + (size_t)(blk - 1) * per : prev_caller;
+        if constexpr (HARD) {
+          r0 = r1 = pv ? (ET)(pv[c_next] & symmask) : (ET)0;
+        } else {
+          r0 = pv ? pv[c_next * NS + e0] : 0.0f;
+          r1 = pv ? pv[c_next * NS + e1] : 0.0f;
+        }
+      }
+      MT tm0, tm1;
+      if constexpr (HARD) {
+        const int32_t d0 = __builtin_popcount(e0 ^ r0), d1 = __builtin_popcount(e1 ^ r1);
+        tm0 = d0 * a.bm1 + (NP - d0) * a.bm0;   // binary-symmetric-channel/stack-decoder.c:266-272
+        tm1 = d1 * a.bm1 + (NP - d1) * a.bm0;
+      } else {
+        tm0 = (float)(1.0 + (double)(a.weight * r0));   // AWGN-channel/stack-decoder.c:274
+        tm1 = (float)(1.0 + (double)(a.weight * r1));
+      }
+      // duplicate_path (:227-241): a free entry, or the least probable one (strict < from +inf)
+      const bool full = size == kStackDepth;
+      const MT mn = row_min(vmin2(vmin2(met[0], met[1]), vmin2(met[2], met[3])));
+      uint32_t c2 = kStackDepth;
+#pragma unroll
+      for (int k = kRowSlots - 1; k >= 0; --k) c2 = met[k] == mn ? (uint32_t)(k * kRowLanes + l) : c2;
+      c2 = row_min_u32(c2);
+      const bool dbad = ext && full && !(mn < hi_sent);
+      bad = bad || dbad;
+      ext = ext && !dbad;
+      const uint32_t lhs = full ? c2 : (uint32_t)size;
+      size += (ext && !full) ? 1 : 0;
+      // extend the current path by input 0 and the duplicate by input 1 (:154-167); when lhs == cur
+      // both extensions apply to the same entry, one after the other
+      const uint32_t n0 = c_next + 1;
+      const uint32_t ns0 = rec.y >> 1, ns1 = ns0 | (1u << (K - 2));
+      const MT m0 = mx + tm0;
+      const bool same = lhs == cur;
+      const uint32_t bn = same ? n0 : c_next;
+      const MT lhs_met = (same ? m0 : mx) + tm1;
+      const uint32_t w1 = bn & 0xFFu;   // outbuf_widx is uint8_t
+      // lane 0 of the row writes the current path's record, lane 1 the duplicate's
+      const bool dup = l == 1;
+      const uint32_t est = dup ? ns1 : ns0;
+      const uint32_t nx = dup ? bn + 1 : n0;
+      const uint32_t bit = dup ? 0x80000000u >> (w1 & 31u) : 0u;
+      const uint32_t p0 = rec.z | (w1 < 32u ? bit : 0u);
+      const uint32_t p1 = rec.w | (w1 >= 32u && w1 < 64u ? bit : 0u);
+      const uint32_t slot = dup ? lhs : (same ? (uint32_t)kStackDepth : cur);
+      const uint32_t es = symbols_of(est);
+      if (ext && l < 2) ent[slot] = make_uint4((nx & 0xFFu) | (es << 8), est, p0, p1);
+      const uint32_t lhs_w = ext ? lhs : 0xFFu, cur_w = (ext && !same) ? cur : 0xFFu;
+#pragma unroll
+      for (int k = 0; k < kRowSlots; ++k) {
+        const uint32_t e = (uint32_t)(k * kRowLanes + l);
+        met[k] = e == lhs_w ? lhs_met : (e == cur_w ? m0 : met[k]);
+      }
+      t += adv ? 1 : 0;
+      const bool finish = bad || t > T;
+      status = bad ? 1 : status;
+      if (finish) {
+        // the most probable path at the end, or entry 0 if the search stopped
+        const uint4 res = status ? ent[0] : rec;
+        const MT m_entry0 = __shfl(met[0], rbase, 64);
+        if (l < OB) {
+          const uint32_t word = l < 4 ? res.z : res.w;
+          const uint32_t byte = (word >> (24 - 8 * (l & 3))) & 0xFFu;
+          a.out[(size_t)blk * OB + l] = (uint8_t)byte;
+          if (a.info && l < IB) {
+            int valid = a.blen - 8 * l;
+            valid = valid > 8 ? 8 : valid;
+            const uint32_t mask = (0xFFu << (8 - valid)) & 0xFFu;
+            errors += __builtin_popcount((byte ^ a.info[(size_t)blk * IB + l]) & mask);
+          }
+        }
+        if constexpr (HARD) {
+          if (l == 0 && a.path_metric) a.path_metric[blk] = status ? m_entry0 : mx;
+        }
+        if (l == 0 && a.status) a.status[blk] = status;
+        blk = fetch();
+        live_row = blk < nb;
+        if (live_row) {
+          stage(blk);
+          t = 1;
+          size = 1;
+          status = 0;
+#pragma unroll
+          for (int k = 0; k < kRowSlots; ++k) met[k] = (k == 0 && l == 0) ? (MT)0 : lo_sent;
+        }
+      }
+    }
+  }
   if (a.err) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) errors += __shfl_xor(errors, off, 64);
