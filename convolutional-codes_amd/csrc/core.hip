@@ -19,6 +19,8 @@
 namespace ccv {
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s);   // stack.hip
 bool stack_rows_eligible(int n, int K, int T);                           // stack.hip
+bool stack_symtab_eligible(int n, int K, int T);                         // stack.hip
+hipError_t launch_stack_symtab(uint16_t* tab, const StackArgs& a, hipStream_t s);   // stack.hip
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s);     // stack.hip
 }
 
@@ -75,7 +77,9 @@ struct ccv_plan {
   int multi_index = -1;              // kMultiCodes index (K = 8, 9), or -1
   bool stack = false;                // stack (sequential) decoder plan
   bool fano = false;                 // Fano decoder plan
-  DeviceBuffer counter;              // Fano: block work counter
+  DeviceBuffer counter;              // Fano, stack rows: block work counter
+  DeviceBuffer symtab;               // stack rows: expected-symbol table (built on first use)
+  bool symtab_ready = false;
   float metric_weight = 0.0f;        // stack, soft: code_param.metric_weight
   int32_t bit_metrics[2] = {0, 0};   // stack, hard: code_param.bit_metrics
   bool step_major = false;           // soft input layout [T][nblocks][2^n] (CCV_FLAG_STEP_MAJOR)
@@ -291,6 +295,7 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->sim_info.release();
   p->sim_out.release();
   p->counter.release();
+  p->symtab.release();
   if (p->d_exp) (void)hipFree(p->d_exp);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -584,6 +589,14 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
     if (p->counter.grow(sizeof(unsigned int), stream)) return -1;
     HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, sizeof(unsigned int), stream));
     a.next_block = static_cast<unsigned int*>(p->counter.ptr);
+    if (ccv::stack_symtab_eligible(a.n, a.K, a.T)) {
+      if (!p->symtab_ready) {   // stream-ordered before this and every later decode on the plan
+        if (p->symtab.grow(sizeof(uint16_t) << (a.K - 1), stream)) return -1;
+        HIP_TRY(ccv::launch_stack_symtab(static_cast<uint16_t*>(p->symtab.ptr), a, stream));
+        p->symtab_ready = true;
+      }
+      a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
+    }
   }
   HIP_TRY(ccv::launch_stack(a, p->d.channel == CCV_HARD, stream));
   return 0;

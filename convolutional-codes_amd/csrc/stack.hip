@@ -25,11 +25,14 @@ static hipError_t launch_pw(const StackArgs& a, size_t lds, hipStream_t s) {
   return launch_v<HARD, PW, 0, false>(a, lds, s);
 }
 
+bool stack_rows_eligible(int n, int K, int T);
+
 // Four searches per wave (stack_decode_rows) as persistent rows: as many waves as the chip holds
 // at once, capped by the blocks (4 per wave).
-template <bool HARD, int NP>
+template <bool HARD, int NP, bool TAB, int RL>
 static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
-  const void* fn = reinterpret_cast<const void*>(&stack_decode_rows<HARD, NP>);
+  constexpr int kStackRows = kStackDepth / RL;   // searches per wave
+  const void* fn = reinterpret_cast<const void*>(&stack_decode_rows<HARD, NP, TAB, RL>);
   const size_t lds = (size_t)kStackRows * stack_rows_row_bytes(a.T, HARD ? 1 : 1 << NP, HARD);
   int dev = 0, cus = 0, per_cu = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -40,8 +43,34 @@ static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
   const long waves_needed = ((long)a.nblocks + kStackRows - 1) / kStackRows;
   const int grid = (int)(waves_needed < resident ? waves_needed : resident);
   if (std::getenv("CCV_STACK_DEBUG"))
-    std::fprintf(stderr, "stack rows: lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n", lds, per_cu, cus, grid);
-  hipLaunchKernelGGL((stack_decode_rows<HARD, NP>), dim3(grid), dim3(kStackDepth), lds, s, a);
+    std::fprintf(stderr, "stack rows: %d lanes per search, table %d, lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n",
+                 RL, (int)TAB, lds, per_cu, cus, grid);
+  hipLaunchKernelGGL((stack_decode_rows<HARD, NP, TAB, RL>), dim3(grid), dim3(kStackDepth), lds, s, a);
+  return hipGetLastError();
+}
+
+template <bool HARD, int NP>
+static hipError_t launch_rows_t(const StackArgs& a, hipStream_t s) {
+  // lanes per search: 16 for soft input (8 lanes would double the LDS per wave -- 4 KiB of symbols
+  // and records per search -- and cap the CU at 9 waves: 519 vs 546 Mbit/s), 8 for hard input
+  // (1152 vs 1073 Mbit/s; profiles/r02c_stack_ab.txt). CCV_STACK_ROWL=8/16 overrides.
+  int rl = HARD ? 8 : 16;
+  if (const char* env = std::getenv("CCV_STACK_ROWL")) rl = std::atoi(env);
+  if (rl == 8) return a.symtab ? launch_rows<HARD, NP, true, 8>(a, s) : launch_rows<HARD, NP, false, 8>(a, s);
+  return a.symtab ? launch_rows<HARD, NP, true, 16>(a, s) : launch_rows<HARD, NP, false, 16>(a, s);
+}
+
+bool stack_symtab_eligible(int n, int K, int T) {
+  if (const char* env = std::getenv("CCV_STACK_SYMTAB"))   // A/B: 0 = parities per iteration
+    if (env[0] == '0') return false;
+  return stack_rows_eligible(n, K, T) && K <= kSymtabMaxK;
+}
+
+hipError_t launch_stack_symtab(uint16_t* tab, const StackArgs& a, hipStream_t s) {
+  const unsigned S = 1u << (a.K - 1);
+  const dim3 grid((S + 255) / 256), block(256);
+  if (a.n == 2) hipLaunchKernelGGL((stack_symtab_init<2>), grid, block, 0, s, tab, a);
+  else hipLaunchKernelGGL((stack_symtab_init<3>), grid, block, 0, s, tab, a);
   return hipGetLastError();
 }
 
@@ -53,8 +82,8 @@ bool stack_rows_eligible(int n, int K, int T) {
 
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
   if (stack_rows_eligible(a.n, a.K, a.T) && a.next_block != nullptr) {
-    if (hard) return a.n == 2 ? launch_rows<true, 2>(a, s) : launch_rows<true, 3>(a, s);
-    return a.n == 2 ? launch_rows<false, 2>(a, s) : launch_rows<false, 3>(a, s);
+    if (hard) return a.n == 2 ? launch_rows_t<true, 2>(a, s) : launch_rows_t<true, 3>(a, s);
+    return a.n == 2 ? launch_rows_t<false, 2>(a, s) : launch_rows_t<false, 3>(a, s);
   }
   const size_t per = (size_t)a.T * (hard ? 1 : ((size_t)1 << a.n));
   const size_t lds = 2 * per * (hard ? 1 : sizeof(float));

@@ -47,6 +47,7 @@ struct StackArgs {
   unsigned long long* err;
   int32_t* status;         // optional [nb]: 0 ok, 1 = the reference would read past its buffers
   unsigned int* next_block;  // stack_decode_rows: work counter, zero before the launch
+  const uint16_t* symtab;    // stack_decode_rows, K <= kSymtabMaxK: [2^(K-1)] expected symbols
 };
 
 constexpr int kStackDepth = 64;   // stack-decoder.c:12 == wave64
@@ -284,40 +285,66 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode(StackArgs a) {
 // Same arithmetic, tie rules and streaming quirks as stack_decode (the previous block's symbols
 // are read from global memory when a path runs ahead of the frontier). K <= 32 (32-bit state),
 // n = NP in {2, 3}, T <= 64 (two path words); other codes use stack_decode.
-constexpr int kStackRows = 4;                        // searches per wave
-constexpr int kRowLanes = kStackDepth / kStackRows;  // 16: one DPP row
-constexpr int kRowSlots = kStackDepth / kRowLanes;   // 4 stack entries per lane
 constexpr int kRowsMaxT = 64;
 
-// row-wide reductions (every lane of the 16-lane row gets the result); explicit s_nop for the
-// VALU-write -> DPP-read hazard, as CCV_WAVE_REDUCE
+// row-wide reductions over RL = 16 or 8 lanes (every lane of the row gets the result); explicit
+// s_nop for the VALU-write -> DPP-read hazard, as CCV_WAVE_REDUCE
 #define CCV_ROW_STEP(op, ctrl) "s_nop 1\n" op "_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf\n"
-#define CCV_ROW_REDUCE(op)                                                                     \
+#define CCV_ROW_REDUCE8(op)                                                                    \
   CCV_ROW_STEP(op, "quad_perm:[1,0,3,2]") CCV_ROW_STEP(op, "quad_perm:[2,3,0,1]")             \
-  CCV_ROW_STEP(op, "row_half_mirror") CCV_ROW_STEP(op, "row_mirror")
-__device__ __forceinline__ float row_max(float v) { asm volatile(CCV_ROW_REDUCE("v_max_f32") : "+v"(v)); return v; }
-__device__ __forceinline__ float row_min(float v) { asm volatile(CCV_ROW_REDUCE("v_min_f32") : "+v"(v)); return v; }
-__device__ __forceinline__ int32_t row_max(int32_t v) { asm volatile(CCV_ROW_REDUCE("v_max_i32") : "+v"(v)); return v; }
-__device__ __forceinline__ int32_t row_min(int32_t v) { asm volatile(CCV_ROW_REDUCE("v_min_i32") : "+v"(v)); return v; }
-__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) { asm volatile(CCV_ROW_REDUCE("v_min_u32") : "+v"(v)); return v; }
+  CCV_ROW_STEP(op, "row_half_mirror")
+#define CCV_ROW_REDUCE(op) CCV_ROW_REDUCE8(op) CCV_ROW_STEP(op, "row_mirror")
+#define CCV_ROW_FN(name, T, op)                                                                 \
+  template <int RL>                                                                             \
+  __device__ __forceinline__ T name(T v) {                                                      \
+    if constexpr (RL == 16) asm volatile(CCV_ROW_REDUCE(op) : "+v"(v));                        \
+    else asm volatile(CCV_ROW_REDUCE8(op) : "+v"(v));                                          \
+    return v;                                                                                   \
+  }
+CCV_ROW_FN(row_max, float, "v_max_f32")
+CCV_ROW_FN(row_min, float, "v_min_f32")
+CCV_ROW_FN(row_max, int32_t, "v_max_i32")
+CCV_ROW_FN(row_min, int32_t, "v_min_i32")
+CCV_ROW_FN(row_min_u32, uint32_t, "v_min_u32")
+#undef CCV_ROW_FN
+#undef CCV_ROW_REDUCE8
 #undef CCV_ROW_REDUCE
 #undef CCV_ROW_STEP
 
-__device__ __forceinline__ float vmax2(float a, float b) { return __builtin_fmaxf(a, b); }
+// max / min without the canonicalising v_max x,x hipcc wraps around fmaxf (IEEE max/min skip NaN,
+// as the reference's strict compares do)
+__device__ __forceinline__ float vmax2(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+__device__ __forceinline__ float vmin2(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
 __device__ __forceinline__ int32_t vmax2(int32_t a, int32_t b) { return a > b ? a : b; }
-__device__ __forceinline__ float vmin2(float a, float b) { return __builtin_fminf(a, b); }
 __device__ __forceinline__ int32_t vmin2(int32_t a, int32_t b) { return a < b ? a : b; }
 
-// LDS bytes per row: the block's symbols (16-byte aligned), then 65 entry records (64 + a dummy)
+// LDS bytes per row: the block's symbols (16-byte aligned), 65 entry records (64 + a dummy), then
+// the 64 path metrics + the dummy (padded to 68)
 __host__ __device__ constexpr size_t stack_rows_sym_bytes(int T, int ns, bool hard) {
   return (((size_t)T * (size_t)ns * (hard ? 1 : 4)) + 15) & ~(size_t)15;
 }
 __host__ __device__ constexpr size_t stack_rows_row_bytes(int T, int ns, bool hard) {
-  return stack_rows_sym_bytes(T, ns, hard) + (size_t)(kStackDepth + 1) * 16;
+  return stack_rows_sym_bytes(T, ns, hard) + (size_t)(kStackDepth + 1) * 16 + 68 * 4;
 }
 
-template <bool HARD, int NP>
+// Expected-symbol table for the rows kernel: entry s = lane_symbols(s) (e0 << 8 | e1), so a new
+// path's symbols are one cached 2-byte load instead of ~25 VALU of parities per search iteration.
+constexpr int kSymtabMaxK = 16;   // 2^15 entries, 64 KiB
+template <int NP>
+__global__ void stack_symtab_init(uint16_t* tab, StackArgs a) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (1u << (a.K - 1))) return;
+  uint64_t poly[kMaxN];
+#pragma unroll
+  for (int k = 0; k < kMaxN; ++k) poly[k] = a.poly[k];
+  tab[s] = (uint16_t)lane_symbols<NP, true>(poly, NP, a.K, a.gen == GEN_REF_X86, (uint64_t)s);
+}
+
+template <bool HARD, int NP, bool TAB, int RL>
 __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
+  static_assert(RL == 16 || RL == 8, "a search is one DPP row or half-row");
+  constexpr int kRowLanes = RL;                        // lanes per search
+  constexpr int kRowSlots = kStackDepth / RL;          // stack entries per lane
   using MT = typename std::conditional<HARD, int32_t, float>::type;
   using ET = typename std::conditional<HARD, uint8_t, float>::type;
   constexpr int NS = HARD ? 1 : (1 << NP);
@@ -331,6 +358,10 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
   unsigned char* rowp = smem + (size_t)(lane / kRowLanes) * stack_rows_row_bytes(T, NS, HARD);
   ET* syms = reinterpret_cast<ET*>(rowp);
   uint4* ent = reinterpret_cast<uint4*>(rowp + sym_bytes);   // [65] records
+  // [68] path metrics; entry e = l * kRowSlots + k, so lane l reads its kRowSlots entries as 16-byte
+  // rows; entries not on the stack hold the low sentinel (never a hit, so the scan needs no liveness
+  // test; the least-probable scan only matters once all 64 are live)
+  MT* metl = reinterpret_cast<MT*>(rowp + sym_bytes + (kStackDepth + 1) * 16);
   const ET* in = reinterpret_cast<const ET*>(a.in);
   const ET* prev_caller = reinterpret_cast<const ET*>(a.prev);
   uint64_t poly[kMaxN];
@@ -342,7 +373,10 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
   const MT hi_sent = HARD ? (MT)INT32_MAX : (MT)__builtin_inff();
   const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
   // record: x = next index | expected symbols (e0 << 8 | e1) << 8, y = encoder state, z/w = path
-  auto symbols_of = [&](uint32_t st) { return lane_symbols<NP, true>(poly, NP, K, idiom, (uint64_t)st); };
+  auto symbols_of = [&](uint32_t st) -> uint32_t {
+    if constexpr (TAB) return a.symtab[st];
+    else return lane_symbols<NP, true>(poly, NP, K, idiom, (uint64_t)st);
+  };
   const uint32_t esym_root = symbols_of(0);
 
   auto fetch = [&]() -> int {
@@ -359,12 +393,11 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       syms[i] = v;
     }
     if (l == 0) ent[0] = make_uint4(esym_root << 8, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < kRowSlots; ++k) metl[l * kRowSlots + k] = (k == 0 && l == 0) ? (MT)0 : lo_sent;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   };
 
-  MT met[kRowSlots];   // entry k * 16 + l; entries not on the stack hold the low sentinel
-#pragma unroll
-  for (int k = 0; k < kRowSlots; ++k) met[k] = (k == 0 && l == 0) ? (MT)0 : lo_sent;
   int blk = fetch();
   bool live_row = blk < nb;
   int t = 1, size = 1, status = 0;
@@ -373,14 +406,18 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
 
   while (__ballot(live_row) != 0) {
     if (live_row) {
-      // get_most_probable_path (stack-decoder.c:213-225): strict > from -inf, first index wins.
-      // Entries not yet on the stack hold -inf / INT32_MIN (never a hit), so the scan needs no
-      // liveness test; the least-probable scan below only matters once all 64 are live.
-      const MT mx = row_max(vmax2(vmax2(met[0], met[1]), vmax2(met[2], met[3])));
+      // get_most_probable_path (stack-decoder.c:213-225): strict > from -inf, first index wins
+      MT met[kRowSlots];
+#pragma unroll
+      for (int k = 0; k < kRowSlots; ++k) met[k] = metl[l * kRowSlots + k];
+      MT mx = met[0];
+#pragma unroll
+      for (int k = 1; k < kRowSlots; ++k) mx = vmax2(mx, met[k]);
+      mx = row_max<RL>(mx);
       uint32_t cand = kStackDepth;
 #pragma unroll
-      for (int k = kRowSlots - 1; k >= 0; --k) cand = met[k] == mx ? (uint32_t)(k * kRowLanes + l) : cand;
-      const uint32_t cur = row_min_u32(cand);
+      for (int k = kRowSlots - 1; k >= 0; --k) cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
+      const uint32_t cur = row_min_u32<RL>(cand);
       const bool ok = mx > lo_sent;
       // the common path is branch-free: every quantity is computed, the outcome selected
       const uint4 rec = ent[ok ? cur : (uint32_t)kStackDepth];
@@ -390,6 +427,12 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       bool ext = !adv && !bad;
       const uint32_t e0 = (rec.x >> 16) & 0xFFu, e1 = (rec.x >> 8) & 0xFFu;
       const uint32_t ci = c_next < (uint32_t)T ? c_next : (uint32_t)T - 1u;
+      // the new paths' expected symbols (lane 0: input 0 of the current path, lane 1: its duplicate
+      // by input 1), loaded here so the latency hides behind the least-probable scan
+      const bool dup = l == 1;
+      const uint32_t ns0 = rec.y >> 1, ns1 = ns0 | (1u << (K - 2));
+      const uint32_t est = dup ? ns1 : ns0;
+      uint32_t es = symbols_of(est);
       ET r0, r1;
       if constexpr (HARD) { r0 = r1 = syms[ci]; }
       else { r0 = syms[ci * NS + e0]; r1 = syms[ci * NS + e1]; }
@@ -414,11 +457,14 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       }
       // duplicate_path (:227-241): a free entry, or the least probable one (strict < from +inf)
       const bool full = size == kStackDepth;
-      const MT mn = row_min(vmin2(vmin2(met[0], met[1]), vmin2(met[2], met[3])));
+      MT mn = met[0];
+#pragma unroll
+      for (int k = 1; k < kRowSlots; ++k) mn = vmin2(mn, met[k]);
+      mn = row_min<RL>(mn);
       uint32_t c2 = kStackDepth;
 #pragma unroll
-      for (int k = kRowSlots - 1; k >= 0; --k) c2 = met[k] == mn ? (uint32_t)(k * kRowLanes + l) : c2;
-      c2 = row_min_u32(c2);
+      for (int k = kRowSlots - 1; k >= 0; --k) c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
+      c2 = row_min_u32<RL>(c2);
       const bool dbad = ext && full && !(mn < hi_sent);
       bad = bad || dbad;
       ext = ext && !dbad;
@@ -427,27 +473,21 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       // extend the current path by input 0 and the duplicate by input 1 (:154-167); when lhs == cur
       // both extensions apply to the same entry, one after the other
       const uint32_t n0 = c_next + 1;
-      const uint32_t ns0 = rec.y >> 1, ns1 = ns0 | (1u << (K - 2));
       const MT m0 = mx + tm0;
       const bool same = lhs == cur;
       const uint32_t bn = same ? n0 : c_next;
       const MT lhs_met = (same ? m0 : mx) + tm1;
       const uint32_t w1 = bn & 0xFFu;   // outbuf_widx is uint8_t
-      // lane 0 of the row writes the current path's record, lane 1 the duplicate's
-      const bool dup = l == 1;
-      const uint32_t est = dup ? ns1 : ns0;
+      // lane 0 of the row writes the current path's record and metric, lane 1 the duplicate's
       const uint32_t nx = dup ? bn + 1 : n0;
       const uint32_t bit = dup ? 0x80000000u >> (w1 & 31u) : 0u;
       const uint32_t p0 = rec.z | (w1 < 32u ? bit : 0u);
       const uint32_t p1 = rec.w | (w1 >= 32u && w1 < 64u ? bit : 0u);
       const uint32_t slot = dup ? lhs : (same ? (uint32_t)kStackDepth : cur);
-      const uint32_t es = symbols_of(est);
-      if (ext && l < 2) ent[slot] = make_uint4((nx & 0xFFu) | (es << 8), est, p0, p1);
-      const uint32_t lhs_w = ext ? lhs : 0xFFu, cur_w = (ext && !same) ? cur : 0xFFu;
-#pragma unroll
-      for (int k = 0; k < kRowSlots; ++k) {
-        const uint32_t e = (uint32_t)(k * kRowLanes + l);
-        met[k] = e == lhs_w ? lhs_met : (e == cur_w ? m0 : met[k]);
+      asm volatile("" : "+v"(es));   // keeps the table load ahead of the branch below
+      if (ext && l < 2) {
+        ent[slot] = make_uint4((nx & 0xFFu) | (es << 8), est, p0, p1);
+        metl[slot] = dup ? lhs_met : m0;
       }
       t += adv ? 1 : 0;
       const bool finish = bad || t > T;
@@ -455,7 +495,7 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       if (finish) {
         // the most probable path at the end, or entry 0 if the search stopped
         const uint4 res = status ? ent[0] : rec;
-        const MT m_entry0 = __shfl(met[0], rbase, 64);
+        const MT m_entry0 = metl[0];
         if (l < OB) {
           const uint32_t word = l < 4 ? res.z : res.w;
           const uint32_t byte = (word >> (24 - 8 * (l & 3))) & 0xFFu;
@@ -478,8 +518,6 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
           t = 1;
           size = 1;
           status = 0;
-#pragma unroll
-          for (int k = 0; k < kRowSlots; ++k) met[k] = (k == 0 && l == 0) ? (MT)0 : lo_sent;
         }
       }
     }

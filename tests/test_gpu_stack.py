@@ -103,6 +103,33 @@ def test_stack_streaming_context_and_error_count(torch_cuda):
     assert not d_st.cpu().numpy().any()
 
 
+@pytest.mark.parametrize("channel", [SOFT, HARD], ids=["soft", "hard"])
+@pytest.mark.parametrize("c", [K15, CODEBOOK[3], CODEBOOK[0]], ids=["k15", "code3", "code0"])
+def test_stack_rows_kernel_vs_wave_kernel(c, channel, monkeypatch):
+    """The four-searches-per-wave kernel (stack_decode_rows, persistent rows pulling blocks from a
+    counter) decodes bit for bit like the one-search-per-wave kernel (CCV_STACK_WAVE=1) and the
+    oracle: fewer blocks than rows, a ragged batch, noise down to 0 dB (deep searches, full stacks,
+    the idiom codes' self-duplication), with path metrics and per-block status."""
+    plan = StackPlan(c, channel)
+    for nb, db, p_ppm, seed in ((1, 2.0, 60000, 1), (3, 0.0, 100000, 2), (517, 1.0, 80000, 3)):
+        if channel == SOFT:
+            _, data = ch.awgn_blocks(c, nb, ch.noise_scaling(db), seed)
+        else:
+            _, data = ch.bsc_blocks(c, nb, p_ppm, seed)
+        monkeypatch.delenv("CCV_STACK_WAVE", raising=False)
+        rows = plan.decode_host(data)
+        monkeypatch.setenv("CCV_STACK_WAVE", "1")
+        wave = plan.decode_host(data)
+        monkeypatch.delenv("CCV_STACK_WAVE")
+        if channel == SOFT:
+            assert np.array_equal(rows, wave)
+            assert np.array_equal(rows, O.stack_soft(_ocode(c), c.metric_weight, data))
+        else:
+            assert np.array_equal(rows[0], wave[0]) and np.array_equal(rows[1], wave[1])
+            ref, ref_pm = O.stack_hard(_ocode(c), c.bit_metrics, data)
+            assert np.array_equal(rows[0], ref) and np.array_equal(rows[1], ref_pm)
+
+
 def test_stack_plan_limits():
     with pytest.raises(Exception, match="uint8_t"):
         StackPlan(K15.with_(blen=250), HARD)          # T = 264 > 255
