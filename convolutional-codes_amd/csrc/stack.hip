@@ -29,10 +29,10 @@ bool stack_rows_eligible(int n, int K, int T);
 
 // Four searches per wave (stack_decode_rows) as persistent rows: as many waves as the chip holds
 // at once, capped by the blocks (4 per wave).
-template <bool HARD, int NP, bool TAB, int RL>
+template <bool HARD, int NP, bool TAB, int RL, bool KEY = false>
 static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
   constexpr int kStackRows = kStackDepth / RL;   // searches per wave
-  const void* fn = reinterpret_cast<const void*>(&stack_decode_rows<HARD, NP, TAB, RL>);
+  const void* fn = reinterpret_cast<const void*>(&stack_decode_rows<HARD, NP, TAB, RL, KEY>);
   const size_t lds = (size_t)kStackRows * stack_rows_row_bytes(a.T, HARD ? 1 : 1 << NP, HARD);
   int dev = 0, cus = 0, per_cu = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -43,19 +43,31 @@ static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
   const long waves_needed = ((long)a.nblocks + kStackRows - 1) / kStackRows;
   const int grid = (int)(waves_needed < resident ? waves_needed : resident);
   if (std::getenv("CCV_STACK_DEBUG"))
-    std::fprintf(stderr, "stack rows: %d lanes per search, table %d, lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n",
-                 RL, (int)TAB, lds, per_cu, cus, grid);
-  hipLaunchKernelGGL((stack_decode_rows<HARD, NP, TAB, RL>), dim3(grid), dim3(kStackDepth), lds, s, a);
+    std::fprintf(stderr, "stack rows: %d lanes per search, table %d, keys %d, lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n",
+                 RL, (int)TAB, (int)KEY, lds, per_cu, cus, grid);
+  hipLaunchKernelGGL((stack_decode_rows<HARD, NP, TAB, RL, KEY>), dim3(grid), dim3(kStackDepth), lds, s, a);
   return hipGetLastError();
 }
 
 template <bool HARD, int NP>
 static hipError_t launch_rows_t(const StackArgs& a, hipStream_t s) {
-  // lanes per search: 16 for soft input (8 lanes would double the LDS per wave -- 4 KiB of symbols
-  // and records per search -- and cap the CU at 9 waves: 519 vs 546 Mbit/s), 8 for hard input
-  // (1152 vs 1073 Mbit/s; profiles/r02c_stack_ab.txt). CCV_STACK_ROWL=8/16 overrides.
-  int rl = HARD ? 8 : 16;
+  // Hard input whose metrics fit a 32-bit key with the entry index (stack_dev.hpp) runs one reduction
+  // per scan. Lanes per search: 16, except hard input without keys: 8 (8 entries per lane, 8 searches
+  // per wave -- fewer DPP steps, but twice the LDS per wave, which for soft input caps a CU at 9 waves).
+  // Measured (profiles/r02c_stack_ab.txt): soft 16 lanes 546 vs 8 lanes 519 Mbit/s; hard keyed
+  // 16 lanes 1275, 8 lanes 1259, unkeyed 8 lanes 1104-1152, 16 lanes 1073. CCV_STACK_ROWL=8/16 and
+  // CCV_STACK_KEYS=0 override.
+  bool keyed = false;
+  if constexpr (HARD) {
+    keyed = a.symtab != nullptr && stack_rows_keyed(a.T, a.n, a.bm0, a.bm1);
+    if (const char* env = std::getenv("CCV_STACK_KEYS")) keyed = keyed && env[0] != '0';
+  }
+  int rl = HARD && !keyed ? 8 : 16;
   if (const char* env = std::getenv("CCV_STACK_ROWL")) rl = std::atoi(env);
+  if (keyed) {
+    if (rl == 8) return launch_rows<HARD, NP, true, 8, HARD>(a, s);
+    return launch_rows<HARD, NP, true, 16, HARD>(a, s);
+  }
   if (rl == 8) return a.symtab ? launch_rows<HARD, NP, true, 8>(a, s) : launch_rows<HARD, NP, false, 8>(a, s);
   return a.symtab ? launch_rows<HARD, NP, true, 16>(a, s) : launch_rows<HARD, NP, false, 16>(a, s);
 }

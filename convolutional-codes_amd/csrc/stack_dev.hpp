@@ -340,9 +340,20 @@ __global__ void stack_symtab_init(uint16_t* tab, StackArgs a) {
   tab[s] = (uint16_t)lane_symbols<NP, true>(poly, NP, a.K, a.gen == GEN_REF_X86, (uint64_t)s);
 }
 
-template <bool HARD, int NP, bool TAB, int RL>
+// KEY (hard input whose path metrics provably stay below 2^24 in magnitude: T * n * max|bit metric|
+// < 2^24, stack_rows_keyed): metric and entry index share one 32-bit key, metric * 64 + index, so
+// each scan is ONE row reduction -- max of metric * 64 + (63 - e) gives the largest metric and, among
+// equal ones, the lowest index; min of metric * 64 + e the smallest and the lowest index. Entries not
+// on the stack then hold -2^25 (a key below every live one).
+__host__ __device__ constexpr bool stack_rows_keyed(int T, int n, int32_t bm0, int32_t bm1) {
+  const long long b0 = bm0 < 0 ? -(long long)bm0 : bm0, b1 = bm1 < 0 ? -(long long)bm1 : bm1;
+  return (long long)T * n * (b0 > b1 ? b0 : b1) < (1ll << 24);
+}
+
+template <bool HARD, int NP, bool TAB, int RL, bool KEY = false>
 __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
   static_assert(RL == 16 || RL == 8, "a search is one DPP row or half-row");
+  static_assert(HARD || !KEY, "keys pack integer metrics");
   constexpr int kRowLanes = RL;                        // lanes per search
   constexpr int kRowSlots = kStackDepth / RL;          // stack entries per lane
   using MT = typename std::conditional<HARD, int32_t, float>::type;
@@ -371,6 +382,7 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
   const uint32_t symmask = (1u << NP) - 1u;
   const MT lo_sent = HARD ? (MT)INT32_MIN : (MT)-__builtin_inff();
   const MT hi_sent = HARD ? (MT)INT32_MAX : (MT)__builtin_inff();
+  const MT dead = KEY ? (MT)-(1 << 25) : lo_sent;   // metric of an entry not on the stack
   const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
   // record: x = next index | expected symbols (e0 << 8 | e1) << 8, y = encoder state, z/w = path
   auto symbols_of = [&](uint32_t st) -> uint32_t {
@@ -394,7 +406,7 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
     }
     if (l == 0) ent[0] = make_uint4(esym_root << 8, 0u, 0u, 0u);
 #pragma unroll
-    for (int k = 0; k < kRowSlots; ++k) metl[l * kRowSlots + k] = (k == 0 && l == 0) ? (MT)0 : lo_sent;
+    for (int k = 0; k < kRowSlots; ++k) metl[l * kRowSlots + k] = (k == 0 && l == 0) ? (MT)0 : dead;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   };
 
@@ -410,15 +422,29 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       MT met[kRowSlots];
 #pragma unroll
       for (int k = 0; k < kRowSlots; ++k) met[k] = metl[l * kRowSlots + k];
-      MT mx = met[0];
+      MT mx;
+      uint32_t cur;
+      bool ok;
+      if constexpr (KEY) {
+        int32_t kx = INT32_MIN;
 #pragma unroll
-      for (int k = 1; k < kRowSlots; ++k) mx = vmax2(mx, met[k]);
-      mx = row_max<RL>(mx);
-      uint32_t cand = kStackDepth;
+        for (int k = 0; k < kRowSlots; ++k)
+          kx = vmax2(kx, (int32_t)((uint32_t)met[k] * 64u) + (63 - (l * kRowSlots + k)));
+        kx = row_max<RL>(kx);
+        mx = (MT)(kx >> 6);
+        cur = 63u - ((uint32_t)kx & 63u);
+        ok = kx > -(1 << 30);
+      } else {
+        mx = met[0];
 #pragma unroll
-      for (int k = kRowSlots - 1; k >= 0; --k) cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
-      const uint32_t cur = row_min_u32<RL>(cand);
-      const bool ok = mx > lo_sent;
+        for (int k = 1; k < kRowSlots; ++k) mx = vmax2(mx, met[k]);
+        mx = row_max<RL>(mx);
+        uint32_t cand = kStackDepth;
+#pragma unroll
+        for (int k = kRowSlots - 1; k >= 0; --k) cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
+        cur = row_min_u32<RL>(cand);
+        ok = mx > lo_sent;
+      }
       // the common path is branch-free: every quantity is computed, the outcome selected
       const uint4 rec = ent[ok ? cur : (uint32_t)kStackDepth];
       const uint32_t c_next = rec.x & 0xFFu;
@@ -457,14 +483,26 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       }
       // duplicate_path (:227-241): a free entry, or the least probable one (strict < from +inf)
       const bool full = size == kStackDepth;
-      MT mn = met[0];
+      MT mn;
+      uint32_t c2;
+      if constexpr (KEY) {
+        int32_t kn = INT32_MAX;
 #pragma unroll
-      for (int k = 1; k < kRowSlots; ++k) mn = vmin2(mn, met[k]);
-      mn = row_min<RL>(mn);
-      uint32_t c2 = kStackDepth;
+        for (int k = 0; k < kRowSlots; ++k)
+          kn = vmin2(kn, (int32_t)((uint32_t)met[k] * 64u) + (l * kRowSlots + k));
+        kn = row_min<RL>(kn);
+        mn = (MT)(kn >> 6);
+        c2 = (uint32_t)kn & 63u;
+      } else {
+        mn = met[0];
 #pragma unroll
-      for (int k = kRowSlots - 1; k >= 0; --k) c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
-      c2 = row_min_u32<RL>(c2);
+        for (int k = 1; k < kRowSlots; ++k) mn = vmin2(mn, met[k]);
+        mn = row_min<RL>(mn);
+        c2 = kStackDepth;
+#pragma unroll
+        for (int k = kRowSlots - 1; k >= 0; --k) c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
+        c2 = row_min_u32<RL>(c2);
+      }
       const bool dbad = ext && full && !(mn < hi_sent);
       bad = bad || dbad;
       ext = ext && !dbad;
