@@ -510,6 +510,21 @@ static int sequential_plan_create(ccv_plan** out, bool fano, int channel, int n,
   return 0;
 }
 
+// The expected-symbol table of the sequential decoders (stack rows kernel, Fano), built on the
+// plan's first decode that uses it, stream-ordered before that and every later decode.
+static int ensure_symtab(ccv_plan* p, hipStream_t stream) {
+  if (p->symtab_ready) return 0;
+  ccv::StackArgs sa{};
+  sa.n = p->d.n;
+  sa.K = p->d.K;
+  sa.gen = p->d.gen_mode;
+  memcpy(sa.poly, p->polys, sizeof sa.poly);
+  if (p->symtab.grow(sizeof(uint16_t) << (sa.K - 1), stream)) return -1;
+  HIP_TRY(ccv::launch_stack_symtab(static_cast<uint16_t*>(p->symtab.ptr), sa, stream));
+  p->symtab_ready = true;
+  return 0;
+}
+
 int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_out,
                            int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
                            uint32_t* d_iterations, void* stream_v) {
@@ -540,6 +555,12 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   a.err = d_info ? d_errors : nullptr;
   a.iterations = d_iterations;
   if (const char* env = std::getenv("CCV_FANO_COUNT_MOVES")) a.count_moves = env[0] == '1';
+  bool tab = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3);
+  if (const char* env = std::getenv("CCV_FANO_SYMTAB")) tab = tab && env[0] != '0';
+  if (tab) {
+    if (ensure_symtab(p, stream)) return -1;
+    a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
+  }
   const bool debug = std::getenv("CCV_FANO_DEBUG") != nullptr;
   if (debug) {   // diagnostics: synchronous, prints lane utilisation
     if (p->counter.grow(32, stream)) return -1;
@@ -590,11 +611,7 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
     HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, sizeof(unsigned int), stream));
     a.next_block = static_cast<unsigned int*>(p->counter.ptr);
     if (ccv::stack_symtab_eligible(a.n, a.K, a.T)) {
-      if (!p->symtab_ready) {   // stream-ordered before this and every later decode on the plan
-        if (p->symtab.grow(sizeof(uint16_t) << (a.K - 1), stream)) return -1;
-        HIP_TRY(ccv::launch_stack_symtab(static_cast<uint16_t*>(p->symtab.ptr), a, stream));
-        p->symtab_ready = true;
-      }
+      if (ensure_symtab(p, stream)) return -1;
       a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
     }
   }

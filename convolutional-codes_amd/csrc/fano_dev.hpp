@@ -47,6 +47,7 @@ struct FanoArgs {
                              // moves (forward, back, threshold relaxations) instead
   unsigned long long* stats; // diagnostics (CCV_FANO_DEBUG): [0] sum over waves of loop passes,
                              // [1] sum over lanes of passes in which the lane had a search to advance
+  const uint16_t* symtab;    // TAB: [2^(K-1)] expected symbols (stack_symtab_init), K <= kSymtabMaxK
 };
 
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
@@ -86,8 +87,11 @@ struct FanoRow<false, NP> {
 // Here every pass of the kernel loop is ONE move -- forward, one step back, or a threshold
 // relaxation -- so all lanes of a wave stay in the same code whatever phase their searches are in,
 // and the branch metrics of the node a lane lands on are computed by one shared piece of code.
-template <bool HARD, int NP, bool W32, int RM>
+// TAB: the node's expected symbols are one cached load from the per-plan table (stack_dev.hpp,
+// stack_symtab_init) instead of ~25 VALU of parities per pass.
+template <bool HARD, int NP, bool W32, int RM, bool TAB = false>
 __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
+  static_assert(!TAB || (W32 && NP != 0), "the table covers specialised K <= 32 codes");
   using MT = typename std::conditional<HARD, int32_t, float>::type;
   using ET = typename std::conditional<HARD, uint8_t, float>::type;
   using ST = typename std::conditional<W32, uint32_t, uint64_t>::type;
@@ -129,7 +133,9 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   // received row is `row` (ROWS): tm0 >= tm1 afterwards, swapped = input 1 is the best branch
   auto node_metrics = [&](const ET* rx, int d, ST st, const FanoRow<HARD, NP>& row, MT& tm0, MT& tm1,
                           uint32_t& swapped) {
-    const uint32_t es = lane_symbols<NP, W32>(poly, n, K, idiom, (uint64_t)st);
+    uint32_t es;
+    if constexpr (TAB) es = a.symtab[(uint32_t)st];
+    else es = lane_symbols<NP, W32>(poly, n, K, idiom, (uint64_t)st);
     const uint32_t e0 = es >> 8, e1 = es & 0xFFu;
     MT t0, t1;
     if constexpr (HARD) {

@@ -117,6 +117,25 @@ hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
 // share, doubling the launch), each lane pulling blocks from the queue.
 template <bool HARD, int NP, bool W32, int RM>
 static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
+  if constexpr (W32 && NP != 0) {   // the expected-symbol table variant, where the plan built one
+    if (a.symtab) {
+      const void* fnt = reinterpret_cast<const void*>(&fano_decode<HARD, NP, W32, RM, true>);
+      if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(fnt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+      }
+      int dev = 0, cus = 0, per_cu = 0;
+      hipError_t e = hipGetDevice(&dev);
+      if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fnt, kFanoThreads, lds);
+      if (e != hipSuccess) return e;
+      const int resident = (cus > 0 ? cus : 1) * (per_cu > 0 ? per_cu : 1);
+      const int waves_needed = (a.nblocks + kFanoThreads - 1) / kFanoThreads;
+      const int grid = waves_needed < resident ? waves_needed : resident;
+      hipLaunchKernelGGL((fano_decode<HARD, NP, W32, RM, true>), dim3(grid), dim3(kFanoThreads), lds, s, a);
+      return hipGetLastError();
+    }
+  }
   const void* fn = reinterpret_cast<const void*>(&fano_decode<HARD, NP, W32, RM>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
