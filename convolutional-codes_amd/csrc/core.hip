@@ -22,6 +22,9 @@ bool stack_rows_eligible(int n, int K, int T);                           // stac
 bool stack_symtab_eligible(int n, int K, int T);                         // stack.hip
 hipError_t launch_stack_symtab(uint16_t* tab, const StackArgs& a, hipStream_t s);   // stack.hip
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s);     // stack.hip
+size_t fano_order_bytes(int nblocks);                                    // stack.hip
+hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
+                             hipStream_t s);                             // stack.hip
 }
 
 namespace {
@@ -79,6 +82,7 @@ struct ccv_plan {
   bool fano = false;                 // Fano decoder plan
   DeviceBuffer counter;              // Fano, stack rows: block work counter
   DeviceBuffer symtab;               // stack rows: expected-symbol table (built on first use)
+  DeviceBuffer order;                // Fano, soft: noisiest-first queue order scratch
   bool symtab_ready = false;
   float metric_weight = 0.0f;        // stack, soft: code_param.metric_weight
   int32_t bit_metrics[2] = {0, 0};   // stack, hard: code_param.bit_metrics
@@ -296,6 +300,7 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->sim_out.release();
   p->counter.release();
   p->symtab.release();
+  p->order.release();
   if (p->d_exp) (void)hipFree(p->d_exp);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -560,6 +565,14 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   if (tab) {
     if (ensure_symtab(p, stream)) return -1;
     a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
+  }
+  // soft input: hand out the noisiest blocks first (fano_dev.hpp, fano_score); CCV_FANO_ORDER=0 off
+  bool order = p->d.channel == CCV_SOFT && (a.n == 2 || a.n == 3) && nblocks > 64;
+  if (const char* env = std::getenv("CCV_FANO_ORDER")) order = order && env[0] != '0';
+  if (order) {
+    const size_t need = ccv::fano_order_bytes(a.nblocks);
+    if (p->order.grow(need, stream)) return -1;
+    HIP_TRY(ccv::launch_fano_order(a, p->order.ptr, p->order.bytes, &a.order, stream));
   }
   const bool debug = std::getenv("CCV_FANO_DEBUG") != nullptr;
   if (debug) {   // diagnostics: synchronous, prints lane utilisation

@@ -48,7 +48,30 @@ struct FanoArgs {
   unsigned long long* stats; // diagnostics (CCV_FANO_DEBUG): [0] sum over waves of loop passes,
                              // [1] sum over lanes of passes in which the lane had a search to advance
   const uint16_t* symtab;    // TAB: [2^(K-1)] expected symbols (stack_symtab_init), K <= kSymtabMaxK
+  const uint32_t* order;     // optional [nb]: the queue hands out block order[q] (noisiest first)
 };
+
+// Queue order for soft input (launch_fano_order): a search's length is set by the noise in its
+// block, and a few blocks run into the 10000 x T timeout; handed out last, such a block holds its
+// lane (and its wave) long after the queue has drained. Score = sum over steps of the distance to
+// the nearest constellation point (the demapper output's minimum), sorted descending so the noisy
+// blocks start first and the short ones fill in around them. Output is per block index, so the order
+// changes nothing but the schedule.
+template <int NS>
+__global__ void fano_score(const float* in, int T, int nblocks, float* key, uint32_t* idx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const float* p = in + (size_t)b * T * NS;
+  float s = 0.0f;
+  for (int t = 0; t < T; ++t) {
+    float m = p[t * NS];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) m = fminf(m, p[t * NS + k]);
+    s += m;
+  }
+  key[b] = s;
+  idx[b] = (uint32_t)b;
+}
 
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
 constexpr int kFanoThreads = 64;
@@ -162,7 +185,15 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   };
 
   // per-lane search state
-  unsigned int b = atomicAdd(a.next_block, 1u);
+  // the next block from the queue (through the noisiest-first order when there is one)
+  unsigned int b = 0;
+  auto take = [&]() -> bool {
+    const unsigned int q = atomicAdd(a.next_block, 1u);
+    if (q >= (unsigned int)a.nblocks) return false;
+    b = a.order ? a.order[q] : q;
+    return true;
+  };
+  const bool first = take();
   int cur = 0, frontier = 0;
   ST st = 0;
   MT mcur = 0, thr = 0, tm0 = 0, tm1 = 0;
@@ -225,7 +256,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   };
 
   uint32_t lane_passes = 0;
-  if (b < (unsigned int)a.nblocks) {
+  if (first) {
   start();
   // One move per pass, computed without branches (a lone lane's search is latency-bound and every
   // taken branch costs the wave an instruction-fetch bubble); stores that a lane does not need go
@@ -278,8 +309,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     cur = ncur;
     if (__builtin_expect(expired || (fwd && ncur == T), 0)) {
       finish(!expired);
-      b = atomicAdd(a.next_block, 1u);
-      if (b >= (unsigned int)a.nblocks) break;
+      if (!take()) break;
       start();
       continue;
     }

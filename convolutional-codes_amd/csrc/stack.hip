@@ -4,6 +4,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <hipcub/hipcub.hpp>
+
 #include "fano_dev.hpp"
 #include "stack_dev.hpp"
 
@@ -188,6 +190,38 @@ hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
   if (rm < 0 || rm > 2) rm = kRowsDirect;
   const size_t lds = node_bytes + (rm == kRowsLds ? row_bytes : 0);
   return hard ? launch_fano_h<true>(a, rm, lds, s) : launch_fano_h<false>(a, rm, lds, s);
+}
+
+// Noisiest-first queue order for the soft Fano decoder (fano_dev.hpp, fano_score): scores, then a
+// descending radix sort of (score, block) pairs. Scratch layout: keys in/out, indices in/out, the
+// sort's temporary storage. A null scratch returns the bytes needed.
+size_t fano_order_bytes(int nblocks) {
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, (const float*)nullptr, (float*)nullptr,
+                                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, nblocks);
+  return 16 * (size_t)nblocks + tmp + 256;
+}
+
+hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
+                             hipStream_t s) {
+  const size_t n = (size_t)a.nblocks;
+  float* k_in = static_cast<float*>(scratch);
+  float* k_out = k_in + n;
+  uint32_t* i_in = reinterpret_cast<uint32_t*>(k_out + n);
+  uint32_t* i_out = i_in + n;
+  void* tmp = reinterpret_cast<void*>(((uintptr_t)(i_out + n) + 255) & ~(uintptr_t)255);
+  size_t tmp_bytes = bytes - (size_t)(static_cast<char*>(tmp) - static_cast<char*>(scratch));
+  const float* in = static_cast<const float*>(a.in);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (a.n == 2) hipLaunchKernelGGL((fano_score<4>), grid, block, 0, s, in, a.T, a.nblocks, k_in, i_in);
+  else if (a.n == 3) hipLaunchKernelGGL((fano_score<8>), grid, block, 0, s, in, a.T, a.nblocks, k_in, i_in);
+  else return hipErrorInvalidValue;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes, k_in, k_out, i_in, i_out, a.nblocks, 0,
+                                                   32, s);
+  *order = i_out;
+  return e;
 }
 
 }  // namespace ccv
