@@ -98,6 +98,35 @@ def test_fano_timeouts_iterations_and_error_count(torch_cuda):
     assert (it < 10000 * c.steps).any()
 
 
+@pytest.mark.parametrize("table", ["1", "0"])
+def test_fano_queue_order_and_symbol_table_change_nothing(torch_cuda, monkeypatch, table):
+    """The noisiest-first queue order (soft input) and the expected-symbol table only change the
+    schedule and where the symbols come from: outputs, error count and every block's search length
+    equal the natural-order run and the oracle (K=15, 2 dB: long searches and timeouts)."""
+    torch = torch_cuda
+    monkeypatch.setenv("CCV_FANO_SYMTAB", table)
+    c = K15
+    nb = 700
+    info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 11)
+    ref = O.fano_soft(_ocode(c), c.fano_metric_weight, rx)
+    plan = FanoPlan(c, SOFT)
+    d_rx = torch.from_numpy(rx).cuda()
+    d_info = torch.from_numpy(info).cuda()
+    runs = []
+    for order in ("1", "0"):
+        monkeypatch.setenv("CCV_FANO_ORDER", order)
+        d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+        d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+        d_it = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        plan.decode_fano_device(d_rx, nb, d_out, d_info=d_info, d_errors=d_err, d_iterations=d_it)
+        torch.cuda.synchronize()
+        runs.append((d_out.cpu().numpy(), int(d_err.item()), d_it.cpu().numpy()))
+    (o1, e1, i1), (o0, e0, i0) = runs
+    assert np.array_equal(o1, ref) and np.array_equal(o0, ref)
+    assert e1 == e0 == ch.count_bit_errors(c, info, o1)
+    assert np.array_equal(i1, i0)
+
+
 def test_fano_plan_limits():
     with pytest.raises(Exception, match="uint8_t"):
         FanoPlan(K15.with_(blen=250), SOFT)           # T = 264 > 255
