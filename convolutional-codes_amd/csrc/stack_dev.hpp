@@ -448,9 +448,13 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       // the common path is branch-free: every quantity is computed, the outcome selected
       const uint4 rec = ent[ok ? cur : (uint32_t)kStackDepth];
       const uint32_t c_next = rec.x & 0xFFu;
-      const bool adv = ok && c_next == (uint32_t)t;          // the path ends at the frontier
+      // the path ends at the frontier: the next symbol arrives (t + 1). The reference then scans
+      // again and finds the same path (no metric changed), now one step behind the frontier, and
+      // extends it -- done here in the same iteration, so an arrival costs no scan of its own.
+      const bool adv = ok && c_next == (uint32_t)t;
+      const int tn = t + (adv ? 1 : 0);
       bool bad = !ok || (!adv && c_next >= (uint32_t)T);     // would read past the input buffer
-      bool ext = !adv && !bad;
+      bool ext = !bad && tn <= T;
       const uint32_t e0 = (rec.x >> 16) & 0xFFu, e1 = (rec.x >> 8) & 0xFFu;
       const uint32_t ci = c_next < (uint32_t)T ? c_next : (uint32_t)T - 1u;
       // the new paths' expected symbols (lane 0: input 0 of the current path, lane 1: its duplicate
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       ET r0, r1;
       if constexpr (HARD) { r0 = r1 = syms[ci]; }
       else { r0 = syms[ci * NS + e0]; r1 = syms[ci * NS + e1]; }
-      if (ext && c_next >= (uint32_t)t) {
+      if (ext && c_next >= (uint32_t)tn) {
         // symbols at or beyond the frontier are still the previous block's (header of stack_decode)
         const ET* pv = blk > 0 ? in + (size_t)(blk - 1) * per : prev_caller;
         if constexpr (HARD) {
@@ -527,7 +531,7 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
         ent[slot] = make_uint4((nx & 0xFFu) | (es << 8), est, p0, p1);
         metl[slot] = dup ? lhs_met : m0;
       }
-      t += adv ? 1 : 0;
+      t = tn;
       const bool finish = bad || t > T;
       status = bad ? 1 : status;
       if (finish) {
