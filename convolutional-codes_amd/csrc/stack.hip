@@ -35,7 +35,9 @@ template <bool HARD, int NP, bool TAB, int RL, bool KEY = false>
 static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
   constexpr int kStackRows = kStackDepth / RL;   // searches per wave
   const void* fn = reinterpret_cast<const void*>(&stack_decode_rows<HARD, NP, TAB, RL, KEY>);
-  const size_t lds = (size_t)kStackRows * stack_rows_row_bytes(a.T, HARD ? 1 : 1 << NP, HARD);
+  size_t lds = (size_t)kStackRows * stack_rows_row_bytes(a.T, HARD ? 1 : 1 << NP, HARD);
+  if (const char* env = std::getenv("CCV_STACK_EXTRA_LDS"))   // occupancy studies: unused LDS per wave
+    lds += (size_t)std::atol(env);
   int dev = 0, cus = 0, per_cu = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
