@@ -132,7 +132,9 @@ int ccv_stack_plan_create(ccv_plan** plan, int channel, int n, int K, int blen, 
 /* Stack decode with the streaming context made explicit: d_prev = the block the same decoder
  * received before block 0 (its input buffer still holds it; NULL = a fresh, zeroed decoder); blocks
  * b > 0 follow block b-1. d_status[nb] (optional): 1 where the reference would have read past its
- * buffers (a degenerate search; the output of that block is then not the reference's). */
+ * buffers (a degenerate search; the output of that block is then not the reference's). For K <= 32,
+ * n in {2, 3} and T <= 64 the call resets the plan's block counter on `stream` and, on the plan's
+ * first such call with K <= 16, builds its expected-symbol table there, before the decode kernel. */
 int ccv_stack_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, const void* d_prev,
                             uint8_t* d_out, int32_t* d_path_metric, const uint8_t* d_info,
                             unsigned long long* d_errors, int32_t* d_status, void* stream);
@@ -146,7 +148,9 @@ int ccv_fano_plan_create(ccv_plan** plan, int channel, int n, int K, int blen, c
                          int gen_mode, float fano_metric_weight, const int32_t* fano_bit_metrics);
 
 /* Fano decode with the per-block search length exported: d_iterations[nb] (optional) = iterations
- * used; 10000 * T means the block hit the reference's timeout. */
+ * used; 10000 * T means the block hit the reference's timeout. Soft input with n in {2, 3} and more
+ * than 64 blocks first scores and sorts the blocks (noisiest first) on `stream`, into plan scratch;
+ * outputs are per block index whatever the order. */
 int ccv_fano_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t* d_out,
                            int32_t* d_path_metric, const uint8_t* d_info, unsigned long long* d_errors,
                            uint32_t* d_iterations, void* stream);
