@@ -8,9 +8,11 @@ zero-tail blocks of 40 info bits each, the demapped AWGN channel output at 4 dB,
 the host with the reference's channel arithmetic and then resident in HBM). One process per GPU;
 frames are sharded across ranks (weak scaling), no collective on the data path.
 
-    python bench.py [--gpus N --steps K --warmup W]           (N>1: launched by torch.distributed.run)
+    python bench.py [--gpus N --steps K --warmup W]
 
-Prints ONE JSON line on rank 0.
+N > 1: one process per GPU. Started as `python bench.py --gpus N` the script re-launches itself under
+torch.distributed.run (ccviterbi/launch.py: a child process, before anything touches the GPU); started
+by torch.distributed.run it reads RANK / LOCAL_RANK / WORLD_SIZE. Prints ONE JSON line on rank 0.
 """
 import argparse
 import ctypes
@@ -38,10 +40,46 @@ def algorithmic_bytes_per_bit(code, soft=True, decisions=True):
     return (code.steps * (step_in + dec) + code.info_bytes) / code.blen
 
 
-def cpu_threads():
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None when unlimited / unreadable."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_cpu_info():
+    """What the host offers this process: nproc, the affinity mask, the cgroup quota, the CPU model
+    and the CPU share the pool grants (OMP_NUM_THREADS: 16 per GPU on the MI355X boxes)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
     env = os.environ.get("OMP_NUM_THREADS")
-    n = int(env) if env and env.isdigit() else (os.cpu_count() or 1)
-    return max(1, min(16, n))
+    return {"nproc": os.cpu_count() or 1, "affinity": affinity, "cgroup_quota": _cgroup_cpu_quota(),
+            "omp_num_threads": int(env) if env and env.isdigit() else None, "model": model}
+
+
+def cpu_threads(info=None):
+    """Every host core this process may use: the affinity mask, capped by the cgroup quota and by the
+    pool's per-GPU CPU share (OMP_NUM_THREADS) where set."""
+    info = info or host_cpu_info()
+    n = info["affinity"]
+    for cap in (info["cgroup_quota"], info["omp_num_threads"]):
+        if cap:
+            n = min(n, cap)
+    return max(1, n)
 
 
 def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi", hard=False):
@@ -114,26 +152,52 @@ def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi", hard=
         diff = set(np.nonzero((out != gpu_out[:nb]).any(axis=1))[0].tolist())
         parity = diff <= starts
     bits = nb * code.blen
+    host = host_cpu_info()
     return {"value": round(bits / secs / 1e6, 4), "unit": "Mbit/s", "cores": threads, "kind": kind,
             "sample": f"{nb} blocks ({bits} info bits) of the benchmark frames, {secs:.2f} s wall on "
                       f"{threads} thread(s), one decoder_input() per trellis step as the reference "
-                      f"driver feeds it; output bit-identical to the GPU's: {parity}"}, parity
+                      f"driver feeds it; output bit-identical to the GPU's: {parity}",
+            "bit_identical": parity, "host": host}, parity
 
 
-def load_pmc_traffic(workload_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def load_pmc(workload_key):
+    """Per-launch PMC figures of this workload's dominant kernel from the committed rocprofv3 passes
+    (profiles/pmc_workloads.json, written by tools/pmc_workload.py): HBM bytes (FETCH_SIZE and
+    WRITE_SIZE passes, calibrated by a device copy), SQ_INSTS_VALU and GRBM_GUI_ACTIVE. {} if absent."""
+    path = os.path.join(REPO, "profiles", "pmc_workloads.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        if d.get("workload_key") == workload_key:
-            return d.get("hbm_bytes_per_launch")
+            return json.load(f).get(workload_key, {})
     except (OSError, ValueError):
-        pass
-    return None
+        return {}
 
 
-def main():
+def valu_fraction(pmc):
+    """Issued VALU wave-instructions over the chip's issue capacity in the same cycles: a wave64 VALU
+    instruction issues over 2 cycles on a 32-lane CDNA4 SIMD (MI355X_MICROARCH.md), so 1,024 SIMDs
+    issue at most 512 per cycle; GRBM_GUI_ACTIVE is the busy cycles summed over the 8 XCDs."""
+    valu, grbm = pmc.get("sq_insts_valu"), pmc.get("grbm_gui_active")
+    if not valu or not grbm:
+        return None
+    return valu / (512.0 * grbm / 8.0)
+
+
+def reduce_over_ranks(dist, wall, kernel_ms, errors, device):
+    """The only exchange of the sharded bench: MAX of the wall and kernel times, SUM of the bit-error
+    counters (one RCCL all-reduce each over xGMI, or gloo on CPU) and an all-gather of every rank's
+    kernel time. Returns (wall, kernel_ms, per_rank_kernel_ms, errors)."""
+    import torch
+    world = dist.get_world_size()
+    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    e = torch.tensor([int(errors)], dtype=torch.int64, device=device)
+    dist.all_reduce(e, op=dist.ReduceOp.SUM)
+    per = [torch.zeros(1, dtype=torch.float64, device=device) for _ in range(world)]
+    dist.all_gather(per, torch.tensor([kernel_ms], dtype=torch.float64, device=device))
+    return float(t[0]), float(t[1]), [round(float(x.item()), 4) for x in per], int(e.item())
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -171,7 +235,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused-channel", action="store_true",
                     help="skip the informational on-device channel + decode measurement")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+
+    # --gpus N > 1 without a launcher: start N ranks under torch.distributed.run as a child process,
+    # before torch (let alone HIP) is touched here
+    from ccviterbi import launch
+    if launch.needs_launch(args.gpus):
+        return launch.relaunch(args.gpus, os.path.abspath(__file__),
+                               sys.argv[1:] if argv is None else list(argv))
+    rank, local_rank, world = launch.world_from_env()
+    launch.check_world(args.gpus, world)
 
     import torch
     import torch.distributed as dist
@@ -179,11 +252,6 @@ def main():
     from ccviterbi import HARD, SOFT, FanoPlan, Plan, StackPlan, channel as ch, named_code
     from ccviterbi.decoder import FLAG_GLOBAL_DECISIONS, FLAG_NO_PERSISTENT, FLAG_STEP_MAJOR
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -294,13 +362,11 @@ def main():
                  "note": "same Philox frames generated on the GPU (encoder, mapper, Box-Muller AWGN, "
                          "demapper fused ahead of the ACS)"}
 
-    counters = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(counters, op=dist.ReduceOp.MAX)
-        dist.all_reduce(errs, op=dist.ReduceOp.SUM)   # the BER counter reduction (RCCL over xGMI)
-    wall, kernel_ms = float(counters[0]), float(counters[1])
-    bits_per_step = world * nb * code.blen
     errors = int(errs.item())
+    per_rank_kernel_ms = [round(kernel_ms, 4)]
+    if world > 1:   # MAX of the timings, SUM of the error counters (RCCL over xGMI)
+        wall, kernel_ms, per_rank_kernel_ms, errors = reduce_over_ranks(dist, wall, kernel_ms, errors, "cuda")
+    bits_per_step = world * nb * code.blen
 
     if rank == 0:
         # SURVEY.md 8(d) prices every decoded bit with its survivor decisions (S/8 bytes per step)
@@ -313,8 +379,16 @@ def main():
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         hbm_achieved = hbm_bpb * nb * code.blen / (kernel_ms * 1e-3) / 1e9
-        workload_key = f"{args.code}:frames{args.frames}:{args.layout}" + (":bsc" if hard else "")
-        traffic = load_pmc_traffic(workload_key)
+        workload_key = workload_key_of(args)
+        pmc = load_pmc(workload_key)
+        traffic = pmc.get("hbm_bytes_per_launch")
+        traffic_frac = traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None
+        valu_frac = valu_fraction(pmc)
+        # the binding resource, from the measured fractions: HBM traffic vs VALU issue
+        if traffic_frac is not None and valu_frac is not None:
+            bound = "valu" if valu_frac > traffic_frac else "hbm"
+        else:
+            bound = "hbm" if not sequential and traffic_frac is not None else "valu"
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu, _ = cpu_baseline(code, rx, d_out.cpu().numpy(), args.cpu_seconds, decoder=args.decoder,
@@ -324,6 +398,7 @@ def main():
             "value": round(bits_per_step * args.steps / wall / 1e6, 2),
             "unit": "Mbit/s",
             "n_gpus": world,
+            "world_size": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
@@ -359,10 +434,11 @@ def main():
                     "errors": errors, "bits": bits_per_step * args.steps,
                     "ber": errors / (bits_per_step * args.steps)},
             "kernel_ms": round(kernel_ms, 4),
+            "per_rank_kernel_ms": per_rank_kernel_ms,
             "clock_warmup_s": args.clock_warmup,
             "pcie_inclusive_mbit_s": round(nb * code.blen / pcie_s / 1e6, 1) if pcie_s else None,
             "roofline": {
-                "bound": "hbm",
+                "bound": bound,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -373,9 +449,14 @@ def main():
                 "hbm_bytes_per_bit": round(hbm_bpb, 4),
                 "hbm_achieved": round(hbm_achieved, 1),
                 "hbm_frac": round(hbm_achieved / HBM_PEAK_GBS, 4),
-                "traffic_frac": (round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                 if traffic else None),
-                "binding_resource": "VALU issue (compare-select, no MFMA; DESIGN.md 4.6)",
+                "traffic_frac": round(traffic_frac, 4) if traffic_frac is not None else None,
+                "valu_frac": round(valu_frac, 4) if valu_frac is not None else None,
+                "clock_ghz": (round(pmc["grbm_gui_active"] / 8 / (pmc["kernel_ns"] * 1e-9) / 1e9, 3)
+                              if pmc.get("grbm_gui_active") and pmc.get("kernel_ns") else None),
+                "pmc_source": pmc.get("source"),
+                "bound_basis": "the larger of traffic_frac (PMC HBM bytes / kernel time / 8 TB/s) and "
+                               "valu_frac (SQ_INSTS_VALU / (512 per cycle x GRBM_GUI_ACTIVE / 8)); "
+                               "frac / achieved / peak stay the SURVEY 8(d) HBM figure",
             },
             "cpu_baseline": cpu,
             "fused_channel": fused,
@@ -385,5 +466,15 @@ def main():
         dist.destroy_process_group()
 
 
+def workload_key_of(args):
+    """Key of this workload in profiles/pmc_workloads.json."""
+    key = f"{args.code}:frames{args.frames}:{args.layout}"
+    if args.decoder != "viterbi":
+        key += ":" + args.decoder
+    if args.channel == "bsc":
+        key += ":bsc"
+    return key
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -72,6 +72,8 @@ def core():
     L.ccv_plan_decision_storage.restype = _i
     L.ccv_plan_kernel_variant.argtypes = [_vp]
     L.ccv_plan_kernel_variant.restype = ctypes.c_char_p
+    L.ccv_plan_persistent_waves.argtypes = [_vp, _i]
+    L.ccv_plan_persistent_waves.restype = _i
     L.ccv_plan_reserve.argtypes = [_vp, _sz]
     L.ccv_plan_reserve.restype = _i
     L.ccv_decode_device.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]

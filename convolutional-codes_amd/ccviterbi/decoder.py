@@ -83,6 +83,13 @@ class Plan:
         """The kernel a decode without decision export runs (ccv_plan_kernel_variant)."""
         return self._lib.ccv_plan_kernel_variant(self._h).decode()
 
+    def persistent_waves(self, fresh: bool = False) -> int:
+        """Grid of the plan's persistent kernel (0 = none); fresh bypasses the per-kernel cache."""
+        w = self._lib.ccv_plan_persistent_waves(self._h, 1 if fresh else 0)
+        if w < 0:
+            raise DecoderError(f"ccv_plan_persistent_waves: {_native.last_error()}")
+        return w
+
     def trellis(self) -> np.ndarray:
         out = np.zeros((self.desc.states, 2), np.uint8)
         self._lib.ccv_plan_trellis(self._h, out.ctypes.data)

@@ -44,7 +44,7 @@ def reference_awgn_bits(ebn0_db: float, blen: int) -> int:
 
 
 def reference_bsc_bits(p_ppm: int, blen: int) -> int:
-    """Bits the reference simulates per BSC point (binary-symmetric-channel/main.c:389-398)."""
+    """Bits the reference simulates per BSC point (binary-symmetric-channel/main.c:145-156)."""
     nb = 20000000
     if p_ppm > 12500:
         nb //= 10
@@ -55,16 +55,24 @@ def reference_bsc_bits(p_ppm: int, blen: int) -> int:
     return nb * blen
 
 
-class GpuFrameDecoder:
-    """Decodes one host frame on the current GPU and returns its bit-error count."""
+DECODERS = ("viterbi", "stack", "fano")
 
-    def __init__(self, code: Code, channel: int, frame_blocks: int, device=None):
+
+def _make_plan(code: Code, channel: int, decoder: str):
+    from .decoder import FanoPlan, Plan, StackPlan
+    return {"viterbi": Plan, "stack": StackPlan, "fano": FanoPlan}[decoder](code, channel)
+
+
+class GpuFrameDecoder:
+    """Decodes one host frame on the current GPU and returns its bit-error count (Viterbi, or the
+    stack / Fano decoder: AWGN-channel/{viterbi,stack,fano}-decoder.c and their BSC twins)."""
+
+    def __init__(self, code: Code, channel: int, frame_blocks: int, device=None, decoder: str = "viterbi"):
         import torch
 
-        from .decoder import Plan
         self.torch = torch
         self.device = torch.device(device if device is not None else "cuda")
-        self.plan = Plan(code, channel)
+        self.plan = _make_plan(code, channel, decoder)
         self.plan.reserve(frame_blocks)
         self.code, self.channel = code, channel
         in_elems = code.steps * ((1 << code.n) if channel == SOFT else 1)
@@ -90,20 +98,32 @@ class GpuFrameDecoder:
 
 class DeviceChannelDecoder:
     """Frames generated AND decoded on the current GPU (ccv_simulate_device): the same Philox frames
-    as the host producers, no host generation and no input traffic."""
+    as the host producers, no host generation and no input traffic. For the stack / Fano decoders
+    the on-device channel writes its output (the demapped floats or the BSC symbols) into one
+    HBM frame buffer that the sequential decoder then reads, with its error count fused."""
 
     def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None,
-                 hard_demap=False):
+                 hard_demap=False, decoder: str = "viterbi"):
         import torch
 
         from .decoder import Plan
         self.torch = torch
         self.device = torch.device(device if device is not None else "cuda")
-        self.plan = Plan(code, channel)
+        self.plan = Plan(code, channel)            # the channel (and, for Viterbi, the decoder)
         self.plan.reserve(frame_blocks)
+        self.seq = None if decoder == "viterbi" else _make_plan(code, channel, decoder)
         self.channel, self.frame_blocks, self.seed = channel, frame_blocks, seed
         self.hard_demap = hard_demap
         self.d_err = torch.zeros(1, dtype=torch.int64, device=self.device)
+        if self.seq is not None:
+            self.seq.reserve(frame_blocks)
+            per_block = code.steps * ((1 << code.n) if channel == SOFT else 1)
+            dt = torch.float32 if channel == SOFT else torch.uint8
+            self.d_ch = torch.empty((frame_blocks, per_block), dtype=dt, device=self.device)
+            self.d_info = torch.empty((frame_blocks, code.info_bytes), dtype=torch.uint8, device=self.device)
+            self.d_out = torch.empty((frame_blocks, code.out_bytes), dtype=torch.uint8, device=self.device)
+            self.d_pm = torch.empty(frame_blocks, dtype=torch.int32, device=self.device)
+            self.d_scratch_err = torch.zeros(1, dtype=torch.int64, device=self.device)
 
     def __call__(self, point: float, first_blocks: Sequence[int]) -> int:
         """Bit errors of the frames starting at `first_blocks` at Eb/N0 (dB) or p_ppm `point`."""
@@ -111,8 +131,16 @@ class DeviceChannelDecoder:
         self.d_err.zero_()
         stream = self.torch.cuda.current_stream(self.device)
         for first in first_blocks:
-            self.plan.simulate_device(self.seed, first, self.frame_blocks, param, d_errors=self.d_err,
-                                      stream=stream, hard_demap=self.hard_demap)
+            if self.seq is None:
+                self.plan.simulate_device(self.seed, first, self.frame_blocks, param, d_errors=self.d_err,
+                                          stream=stream, hard_demap=self.hard_demap)
+                continue
+            self.plan.simulate_device(self.seed, first, self.frame_blocks, param,
+                                      d_errors=self.d_scratch_err, d_info=self.d_info,
+                                      d_channel=self.d_ch, stream=stream, hard_demap=self.hard_demap)
+            self.seq.decode_device(self.d_ch, self.frame_blocks, self.d_out,
+                                   d_path_metric=self.d_pm if self.channel == HARD else None,
+                                   d_info=self.d_info, d_errors=self.d_err, stream=stream)
         return int(self.d_err.item())
 
 
@@ -121,25 +149,31 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
               seed: int = 0xC0DE, rank: int = 0, world: int = 1,
               decode: Optional[Callable[[np.ndarray, np.ndarray], int]] = None,
               threads: Optional[int] = None, reduce: bool = True,
-              device_channel: bool = False, hard_demap: bool = False) -> List[BerPoint]:
+              device_channel: bool = False, hard_demap: bool = False,
+              decoder: str = "viterbi", point_index: int = 0,
+              device_decoder: Optional["DeviceChannelDecoder"] = None) -> List[BerPoint]:
     """BER at each point; `decode(info, data) -> errors` defaults to the GPU decoder. With
-    device_channel the frames are generated on the GPU as well (DeviceChannelDecoder)."""
+    device_channel the frames are generated on the GPU as well (DeviceChannelDecoder, or the one
+    passed as `device_decoder`). Point k of `points` draws the Philox stream of point
+    point_index + k, so a sweep split into calls gives the same frames."""
     if bits_per_point is None:
         if channel == SOFT:
             bits_per_point = lambda p: reference_awgn_bits(p, code.blen)   # noqa: E731
         else:
             bits_per_point = lambda p: reference_bsc_bits(int(p), code.blen)  # noqa: E731
-    dev = DeviceChannelDecoder(code, channel, frame_blocks, seed, hard_demap=hard_demap) \
-        if device_channel else None
+    dev = device_decoder
+    if dev is None and device_channel and decode is None:
+        dev = DeviceChannelDecoder(code, channel, frame_blocks, seed, hard_demap=hard_demap, decoder=decoder)
     if decode is None and dev is None:
-        decode = GpuFrameDecoder(code, channel, frame_blocks)
+        decode = GpuFrameDecoder(code, channel, frame_blocks, decoder=decoder)
     counters = np.zeros((len(points), 2), np.int64)
-    for pi, p in enumerate(points):
+    for row, p in enumerate(points):
+        pi = point_index + row   # the point's Philox stream: (seed, pi << 40 | block)
         nframes = max(1, math.ceil(bits_per_point(p) / (frame_blocks * code.blen)))
         if dev is not None:
             mine = range(rank, nframes, world)
-            counters[pi, 0] += dev(p, [(pi << 40) + f * frame_blocks for f in mine])
-            counters[pi, 1] += len(mine) * frame_blocks * code.blen
+            counters[row, 0] += dev(p, [(pi << 40) + f * frame_blocks for f in mine])
+            counters[row, 1] += len(mine) * frame_blocks * code.blen
             continue
         for f in range(rank, nframes, world):
             first = (pi << 40) + f * frame_blocks
@@ -149,8 +183,8 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
             else:
                 info, data = ch.bsc_blocks(code, frame_blocks, int(p), seed, first_block=first,
                                            threads=threads)
-            counters[pi, 0] += decode(info, data)
-            counters[pi, 1] += frame_blocks * code.blen
+            counters[row, 0] += decode(info, data)
+            counters[row, 1] += frame_blocks * code.blen
     if reduce and world > 1:
         counters = all_reduce_counters(counters)
     return [BerPoint(float(p), int(e), int(b)) for p, (e, b) in zip(points, counters)]
@@ -164,3 +198,144 @@ def all_reduce_counters(counters: np.ndarray) -> np.ndarray:
     t = torch.from_numpy(np.ascontiguousarray(counters, np.int64)).to(dev)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.cpu().numpy()
+
+
+def ber_interval(errors: int, bits: int, z: float = 3.29, burst: float = 1.0):
+    """Two-sided interval for the BER behind `errors` of `bits`: Wilson's binomial score interval with
+    the variance inflated by `burst` (decoder errors come in bursts inside a block, so the counts are
+    over-dispersed against independent bits); z = 3.29 is 99.9 %."""
+    if bits <= 0:
+        return (0.0, 1.0)
+    n = bits / burst
+    p = errors / bits
+    z2 = z * z
+    den = 1.0 + z2 / n
+    mid = (p + z2 / (2 * n)) / den
+    half = z * math.sqrt(p * (1 - p) / n + z2 / (4 * n * n)) / den
+    return (max(0.0, mid - half), min(1.0, mid + half))
+
+
+def _parse_points(text: Optional[str], channel: int) -> List[float]:
+    if not text:
+        return list(ch.REFERENCE_EBN0_DB if channel == SOFT else ch.REFERENCE_P_PPM)
+    return [float(x) for x in text.split(",") if x.strip()]
+
+
+def main(argv=None, decode=None):
+    """Sharded BER sweep CLI: `python -m ccviterbi.sim [--gpus N] ...` prints one JSON line per point
+    on rank 0 (the reference drivers print one BER line per point, AWGN-channel/main.c:233,
+    binary-symmetric-channel/main.c:175). `decode(info, data) -> errors` replaces the GPU decoder
+    (tests: the oracle under gloo)."""
+    import argparse
+    import json
+    import os
+    import sys
+    import time
+
+    from . import launch
+    from .code import named_code
+
+    ap = argparse.ArgumentParser(prog="python -m ccviterbi.sim", description=main.__doc__)
+    ap.add_argument("--code", default="code0", help="k7, k9, code0..code5 / wspr, suffix :true = true parity")
+    ap.add_argument("--channel", choices=("awgn", "bsc"), default="awgn")
+    ap.add_argument("--decoder", choices=DECODERS, default="viterbi")
+    ap.add_argument("--points", default=None,
+                    help="comma-separated Eb/N0 dB (awgn) or p in ppm (bsc); default the reference sweep "
+                         "(AWGN-channel/main.c:150-161, binary-symmetric-channel/main.c:103-109)")
+    ap.add_argument("--bits", type=float, default=None,
+                    help="info bits per point (default: the reference's schedule, AWGN-channel/main.c:202-211, "
+                         "binary-symmetric-channel/main.c:145-156)")
+    ap.add_argument("--bits-scale", type=float, default=1.0, help="multiply the reference schedule")
+    ap.add_argument("--frame-blocks", type=int, default=25000, help="blocks per frame (25,000 = 1 M bits)")
+    ap.add_argument("--seed", type=int, default=0xC0DE)
+    ap.add_argument("--device-channel", action="store_true",
+                    help="generate the frames on the GPU (encoder, mapper, Philox AWGN / BSC, demapper)")
+    ap.add_argument("--hard-demap", action="store_true", help="common/hard-demapper.c instead of demapper.c")
+    ap.add_argument("--threads", type=int, default=None, help="host producer threads per rank")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); self-launches torchrun")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
+                    help="process-group backend (default nccl = RCCL over xGMI)")
+    ap.add_argument("--out", default=None, help="also write the points as a JSON list (rank 0)")
+    args = ap.parse_args(argv)
+
+    if launch.needs_launch(args.gpus):
+        return launch.relaunch(args.gpus, "ccviterbi.sim", sys.argv[1:] if argv is None else list(argv),
+                               module=True)
+    rank, local_rank, world = launch.world_from_env()
+    launch.check_world(args.gpus, world)
+    code = named_code(args.code)
+    channel = HARD if args.channel == "bsc" else SOFT
+    if args.hard_demap and channel != SOFT:
+        raise SystemExit("--hard-demap belongs to the AWGN channel")
+    points = _parse_points(args.points, channel)
+    backend = args.backend or ("gloo" if decode is not None else "nccl")
+
+    import torch
+    import torch.distributed as dist
+    if backend == "nccl" or decode is None:
+        torch.cuda.set_device(local_rank)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
+
+    if args.bits is not None:
+        bits_fn = lambda p: int(args.bits)   # noqa: E731
+    elif channel == SOFT:
+        bits_fn = lambda p: int(reference_awgn_bits(p, code.blen) * args.bits_scale)   # noqa: E731
+    else:
+        bits_fn = lambda p: int(reference_bsc_bits(int(p), code.blen) * args.bits_scale)   # noqa: E731
+
+    # the decoder is built once; each point runs locally, then ONE all-reduce (sum) of the whole
+    # [points][errors, bits] table and one MAX of the per-point times
+    dev = gpu = None
+    if decode is None:
+        if args.device_channel:
+            dev = DeviceChannelDecoder(code, channel, args.frame_blocks, args.seed,
+                                       hard_demap=args.hard_demap, decoder=args.decoder)
+        else:
+            gpu = GpuFrameDecoder(code, channel, args.frame_blocks, decoder=args.decoder)
+    counters = np.zeros((len(points), 2), np.int64)
+    secs = np.zeros(len(points), np.float64)
+    for k, p in enumerate(points):
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        (pt,) = ber_sweep(code, [p], channel, bits_per_point=bits_fn, frame_blocks=args.frame_blocks,
+                          seed=args.seed, rank=rank, world=world, decode=decode or gpu,
+                          threads=args.threads, reduce=False, hard_demap=args.hard_demap,
+                          decoder=args.decoder, point_index=k, device_decoder=dev)
+        secs[k] = time.perf_counter() - t0
+        counters[k] = (pt.errors, pt.bits)
+    if world > 1:
+        counters = all_reduce_counters(counters)
+        t = torch.from_numpy(secs).to("cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        secs = t.cpu().numpy()
+    results = []
+    for k, p in enumerate(points):
+        errors, bits = int(counters[k, 0]), int(counters[k, 1])
+        lo, hi = ber_interval(errors, bits)
+        rec = {"code": code.name or args.code, "n": code.n, "K": code.K, "blen": code.blen,
+               "generator": "ref-x86" if code.gen_mode == 0 else "true-parity",
+               "channel": args.channel + ("-hard-demap" if args.hard_demap else ""),
+               "decoder": args.decoder, ("ebn0_db" if channel == SOFT else "p_ppm"): p,
+               "errors": errors, "bits": bits, "ber": errors / bits if bits else None,
+               "ber_99.9_binomial": [lo, hi], "seconds": round(float(secs[k]), 4),
+               "mbit_s": round(bits / secs[k] / 1e6, 1) if secs[k] > 0 else None,
+               "world_size": world, "device_channel": bool(args.device_channel)}
+        results.append(rec)
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+    if rank == 0 and args.out:
+        os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+        with open(args.out, "w") as f:
+            json.dump(results, f, indent=1)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -30,7 +30,9 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <mutex>
 #include <utility>
+#include <vector>
 
 #include "acs_reg.hpp"
 
@@ -601,18 +603,43 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
 // ------------------------------------------------------------------------------------------------
 // Host side: persistent grids hold exactly the resident waves.
 // Resident waves of a one-wave-per-workgroup kernel on the current device (occupancy x CUs), cached
-// per kernel and device.
+// per (kernel, device): every persistent kernel has the type void(*)(RegArgs, int), so the key is the
+// kernel's address, not its type. The table is process-wide (one definition across translation
+// units) and guarded for plans driven from several host threads.
+struct ResidentCache {
+  std::mutex mu;
+  struct Entry { const void* kernel; int dev; int waves; };
+  std::vector<Entry> entries;
+};
+inline ResidentCache& resident_cache() {
+  static ResidentCache c;
+  return c;
+}
+
+// Introspection (ccv_plan_persistent_waves): while `active`, launch_persistent launches nothing and
+// reports the grid it would use -- the cached value, or with `fresh` a new occupancy query.
+struct PersistQuery {
+  bool active = false;
+  bool fresh = false;
+  int waves = 0;
+};
+inline thread_local PersistQuery g_persist_query;
+
 template <class Kern>
-inline int resident_groups(Kern kernel) {
-  static int cached[64] = {};
+inline int resident_groups(Kern kernel, bool fresh = false) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cached[dev] > 0) return cached[dev];
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const void* key = reinterpret_cast<const void*>(kernel);
+  ResidentCache& cache = resident_cache();
+  std::lock_guard<std::mutex> lock(cache.mu);
+  if (!fresh)
+    for (const auto& e : cache.entries)
+      if (e.kernel == key && e.dev == dev) return e.waves;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kRegThreads, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  // CCV_PERSIST_WAVES_PER_CU caps the resident waves per CU (occupancy studies)
+  // CCV_PERSIST_WAVES_PER_CU caps the resident waves per CU (occupancy studies); read per kernel
   if (const char* env = std::getenv("CCV_PERSIST_WAVES_PER_CU")) {
     const int cap = std::atoi(env);
     if (cap > 0 && cap < per_cu) per_cu = cap;
@@ -620,12 +647,16 @@ inline int resident_groups(Kern kernel) {
   // every wave walks the same number of groups: the same number of waves on each of a CU's four
   // SIMDs, or the SIMDs holding one more wave finish a third later (10 per CU: 0.50 vs 0.39 ms)
   if (per_cu >= 4) per_cu -= per_cu % 4;
-  cached[dev] = per_cu * cus;
-  return cached[dev];
+  if (!fresh) cache.entries.push_back({key, dev, per_cu * cus});
+  return per_cu * cus;
 }
 
 template <class Kern>
 inline hipError_t launch_persistent(Kern kernel, const RegArgs& a, int ngroups, hipStream_t stream) {
+  if (g_persist_query.active) {
+    g_persist_query.waves = resident_groups(kernel, g_persist_query.fresh);
+    return hipSuccess;
+  }
   if (ngroups <= 0) return hipSuccess;
   int resident = resident_groups(kernel);
   if (resident <= 0) return hipErrorInvalidDeviceFunction;

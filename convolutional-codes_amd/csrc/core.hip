@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "acs_generic.hpp"
+#include "acs_persist.hpp"
 #include "channel_dev.hpp"
 #include "fano_dev.hpp"
 #include "stack_dev.hpp"
@@ -334,6 +335,19 @@ const char* ccv_plan_kernel_variant(const ccv_plan* p) {
   if (persist_kernel(*p, false)) return "persistent";
   if (p->multi_index >= 0) return regdec_kernel(*p, false) ? "multilane-regdec" : "multilane";
   return regdec_kernel(*p, false) ? "register-regdec" : "register";
+}
+
+int ccv_plan_persistent_waves(const ccv_plan* p, int fresh) {
+  if (!p) return fail("null plan");
+  const ccv::RegLaunchFn persist = persist_kernel(*p, false);
+  if (!persist) return 0;
+  ccv::g_persist_query = ccv::PersistQuery{true, fresh != 0, 0};
+  ccv::RegArgs a{};
+  const hipError_t e = persist(a, 1, nullptr);
+  const int waves = ccv::g_persist_query.waves;
+  ccv::g_persist_query = ccv::PersistQuery{};
+  if (e != hipSuccess) return fail("persistent kernel query: %s", hipGetErrorString(e));
+  return waves;
 }
 
 int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {

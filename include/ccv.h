@@ -91,6 +91,11 @@ int ccv_plan_decision_storage(const ccv_plan* plan);
  * "register-regdec", "register", "multilane-regdec", "multilane", "generic", "stack" or "fano". */
 const char* ccv_plan_kernel_variant(const ccv_plan* plan);
 
+/* Grid (resident waves = occupancy x CUs, whole SIMDs) of the plan's persistent kernel: the value
+ * cached per (kernel, device) that its launches use, or with fresh != 0 a new occupancy query that
+ * bypasses the cache. 0 when the plan runs no persistent kernel, -1 on error. */
+int ccv_plan_persistent_waves(const ccv_plan* plan, int fresh);
+
 /* Grow the plan's device scratch so decodes of up to max_blocks blocks allocate nothing. */
 int ccv_plan_reserve(ccv_plan* plan, size_t max_blocks);
 

@@ -273,6 +273,28 @@ def test_persistent_many_groups_per_wave(torch_cuda, gen, channel):
         assert np.array_equal(pm[idx], ref_pm)
 
 
+def test_persistent_grid_per_kernel(torch_cuda):
+    """The resident-wave grid is cached per KERNEL (all persistent kernels share one C++ type): after
+    K=7 soft, code 0 hard and K=9 soft decode in one process, in that order, each plan's launches use
+    its own kernel's occupancy, not the first kernel's."""
+    torch = torch_cuda
+    plans = [(K7, SOFT), (CODEBOOK[0], HARD), (K9, SOFT)]
+    for c, channel in plans:
+        p = Plan(c, channel)
+        assert p.variant == "persistent"
+        nb = 3 * 64 + 5
+        if channel == SOFT:
+            info, data = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 5)
+        else:
+            info, data = ch.bsc_blocks(c, nb, 40000, 5)
+        out = p.decode_host(data)
+        out = out[0] if channel == HARD else out
+        assert np.array_equal(out, _oracle(c, channel, data)[0])
+        cached, fresh = p.persistent_waves(), p.persistent_waves(fresh=True)
+        assert cached > 0 and cached == fresh, (c.name, channel, cached, fresh)
+    assert Plan(CODEBOOK[0], SOFT, FLAG_NO_PERSISTENT).persistent_waves() == 0
+
+
 def test_dropped_plans_release_device_memory(torch_cuda):
     """Plan.__del__ destroys the plan: creating and dropping plans with large HBM decision scratch
     does not leak device memory (nor streams)."""

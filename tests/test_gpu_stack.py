@@ -130,6 +130,50 @@ def test_stack_rows_kernel_vs_wave_kernel(c, channel, monkeypatch):
             assert np.array_equal(rows[0], ref) and np.array_equal(rows[1], ref_pm)
 
 
+K20 = Code(2, 20, 30, (0xB5A39 << 44, 0xE4C6D << 44), metric_weight=-7.0, bit_metrics=(1, -11),
+           name="k20_custom")   # K in [17, 32], T = 49 <= 64: rows kernel WITHOUT the symbol table
+ROWS_VARIANTS = [
+    ("k20_notab_soft", K20, SOFT, {}),
+    ("k20_notab_hard", K20, HARD, {}),
+    ("k15_hard_unkeyed_rl8", K15, HARD, {"CCV_STACK_KEYS": "0"}),
+    ("k15_hard_unkeyed_rl16", K15, HARD, {"CCV_STACK_KEYS": "0", "CCV_STACK_ROWL": "16"}),
+    ("k15_hard_keyed_rl8", K15, HARD, {"CCV_STACK_ROWL": "8"}),
+    ("k15_soft_rl8", K15, SOFT, {"CCV_STACK_ROWL": "8"}),
+    ("k15_soft_parities", K15, SOFT, {"CCV_STACK_SYMTAB": "0"}),
+    # bit metrics too large for the 32-bit metric/index key: the unkeyed 8-lane default
+    ("code3_hard_bigmetric", CODEBOOK[3].with_(bit_metrics=(1, -200000)), HARD, {}),
+]
+
+
+@pytest.mark.parametrize("name,c,channel,env", ROWS_VARIANTS, ids=[v[0] for v in ROWS_VARIANTS])
+def test_stack_rows_kernel_variants_vs_oracle(name, c, channel, env, monkeypatch):
+    """Every rows-kernel variant the dispatcher can select (stack.hip launch_rows_t): no symbol table
+    (17 <= K <= 32, lane_symbols in the kernel), unkeyed hard scans with the lo_sent sentinel at 8 and
+    16 lanes per search, keyed at 8 lanes, soft at 8 lanes, per-iteration parities -- against the
+    oracle and the one-search-per-wave kernel, with path metrics."""
+    for k in ("CCV_STACK_KEYS", "CCV_STACK_ROWL", "CCV_STACK_SYMTAB", "CCV_STACK_WAVE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    plan = StackPlan(c, channel)
+    for nb, db, p_ppm, seed in ((1, 2.0, 60000, 11), (261, 1.0, 80000, 12)):
+        if channel == SOFT:
+            _, data = ch.awgn_blocks(c, nb, ch.noise_scaling(db), seed)
+        else:
+            _, data = ch.bsc_blocks(c, nb, p_ppm, seed)
+        rows = plan.decode_host(data)
+        monkeypatch.setenv("CCV_STACK_WAVE", "1")
+        wave = plan.decode_host(data)
+        monkeypatch.delenv("CCV_STACK_WAVE")
+        if channel == SOFT:
+            assert np.array_equal(rows, O.stack_soft(_ocode(c), c.metric_weight, data))
+            assert np.array_equal(rows, wave)
+        else:
+            ref, ref_pm = O.stack_hard(_ocode(c), c.bit_metrics, data)
+            assert np.array_equal(rows[0], ref) and np.array_equal(rows[1], ref_pm)
+            assert np.array_equal(rows[0], wave[0]) and np.array_equal(rows[1], wave[1])
+
+
 def test_stack_plan_limits():
     with pytest.raises(Exception, match="uint8_t"):
         StackPlan(K15.with_(blen=250), HARD)          # T = 264 > 255
