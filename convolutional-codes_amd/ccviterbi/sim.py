@@ -5,9 +5,9 @@ The reference streams one block at a time through encoder -> channel -> decoder 
 errors in the decoded callback. Here a sweep point is a set of FRAMES (frame_blocks independent
 blocks each); block b of frame f at point p draws its randomness from the Philox stream
 (seed, p << 40 | f * frame_blocks + b), so results do not depend on how frames are spread over
-processes. Rank r of a world of W processes (one per GPU) takes frames f = r, r+W, ...; each frame is
-produced on the host (libccv_sim), decoded on the GPU with the bit-error count fused into the
-traceback, and at the end ONE all-reduce (sum, int64) of the (errors, bits) counters goes over
+processes. Rank r of a world of W processes (one per GPU) takes the contiguous frame range
+[r*F/W, (r+1)*F/W) of the point's F frames; each frame is produced on the host (libccv_sim) or on the
+GPU (ccv_simulate_device), decoded on the GPU with the bit-error count fused into the traceback, and at the end ONE all-reduce (sum, int64) of the (errors, bits) counters goes over
 torch.distributed (RCCL over xGMI with the nccl backend, gloo on CPU).
 """
 import math
@@ -98,50 +98,62 @@ class GpuFrameDecoder:
 
 class DeviceChannelDecoder:
     """Frames generated AND decoded on the current GPU (ccv_simulate_device): the same Philox frames
-    as the host producers, no host generation and no input traffic. For the stack / Fano decoders
-    the on-device channel writes its output (the demapped floats or the BSC symbols) into one
-    HBM frame buffer that the sequential decoder then reads, with its error count fused."""
+    as the host producers, no host generation and no input traffic. A rank's frames are contiguous
+    blocks of the point's Philox stream, so they go to the device in chunks of `chunk_blocks` (104
+    frames for the Viterbi kernels: enough groups for every resident wave). For the stack / Fano
+    decoders the on-device channel writes its output (the demapped floats or the BSC symbols) into one
+    HBM chunk buffer that the sequential decoder then reads, with its error count fused."""
 
     def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None,
-                 hard_demap=False, decoder: str = "viterbi"):
+                 hard_demap=False, decoder: str = "viterbi", chunk_blocks: Optional[int] = None):
         import torch
 
         from .decoder import Plan
         self.torch = torch
         self.device = torch.device(device if device is not None else "cuda")
+        if chunk_blocks is None:
+            chunk_blocks = frame_blocks * max(1, (2_600_000 if decoder == "viterbi" else 200_000) // frame_blocks)
+        self.chunk = chunk_blocks
         self.plan = Plan(code, channel)            # the channel (and, for Viterbi, the decoder)
-        self.plan.reserve(frame_blocks)
+        self.plan.reserve(self.chunk)
         self.seq = None if decoder == "viterbi" else _make_plan(code, channel, decoder)
         self.channel, self.frame_blocks, self.seed = channel, frame_blocks, seed
         self.hard_demap = hard_demap
         self.d_err = torch.zeros(1, dtype=torch.int64, device=self.device)
         if self.seq is not None:
-            self.seq.reserve(frame_blocks)
+            self.seq.reserve(self.chunk)
             per_block = code.steps * ((1 << code.n) if channel == SOFT else 1)
             dt = torch.float32 if channel == SOFT else torch.uint8
-            self.d_ch = torch.empty((frame_blocks, per_block), dtype=dt, device=self.device)
-            self.d_info = torch.empty((frame_blocks, code.info_bytes), dtype=torch.uint8, device=self.device)
-            self.d_out = torch.empty((frame_blocks, code.out_bytes), dtype=torch.uint8, device=self.device)
-            self.d_pm = torch.empty(frame_blocks, dtype=torch.int32, device=self.device)
+            self.d_ch = torch.empty((self.chunk, per_block), dtype=dt, device=self.device)
+            self.d_info = torch.empty((self.chunk, code.info_bytes), dtype=torch.uint8, device=self.device)
+            self.d_out = torch.empty((self.chunk, code.out_bytes), dtype=torch.uint8, device=self.device)
+            self.d_pm = torch.empty(self.chunk, dtype=torch.int32, device=self.device)
             self.d_scratch_err = torch.zeros(1, dtype=torch.int64, device=self.device)
 
-    def __call__(self, point: float, first_blocks: Sequence[int]) -> int:
-        """Bit errors of the frames starting at `first_blocks` at Eb/N0 (dB) or p_ppm `point`."""
+    def __call__(self, point: float, first_block: int, nblocks: int) -> int:
+        """Bit errors of blocks first_block .. first_block + nblocks - 1 at Eb/N0 (dB) or p_ppm `point`."""
         param = ch.noise_scaling(point) if self.channel == SOFT else int(point)
         self.d_err.zero_()
         stream = self.torch.cuda.current_stream(self.device)
-        for first in first_blocks:
+        for first in range(first_block, first_block + nblocks, self.chunk):
+            nb = min(self.chunk, first_block + nblocks - first)
             if self.seq is None:
-                self.plan.simulate_device(self.seed, first, self.frame_blocks, param, d_errors=self.d_err,
+                self.plan.simulate_device(self.seed, first, nb, param, d_errors=self.d_err,
                                           stream=stream, hard_demap=self.hard_demap)
                 continue
-            self.plan.simulate_device(self.seed, first, self.frame_blocks, param,
+            self.plan.simulate_device(self.seed, first, nb, param,
                                       d_errors=self.d_scratch_err, d_info=self.d_info,
                                       d_channel=self.d_ch, stream=stream, hard_demap=self.hard_demap)
-            self.seq.decode_device(self.d_ch, self.frame_blocks, self.d_out,
+            self.seq.decode_device(self.d_ch, nb, self.d_out,
                                    d_path_metric=self.d_pm if self.channel == HARD else None,
                                    d_info=self.d_info, d_errors=self.d_err, stream=stream)
         return int(self.d_err.item())
+
+
+def shard(nframes: int, rank: int, world: int) -> range:
+    """Rank r's frames: a contiguous range (the per-block Philox stream makes the totals independent
+    of how frames are spread; contiguous ranges let the on-device channel take them in one call)."""
+    return range(nframes * rank // world, nframes * (rank + 1) // world)
 
 
 def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
@@ -170,12 +182,13 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
     for row, p in enumerate(points):
         pi = point_index + row   # the point's Philox stream: (seed, pi << 40 | block)
         nframes = max(1, math.ceil(bits_per_point(p) / (frame_blocks * code.blen)))
+        mine = shard(nframes, rank, world)
         if dev is not None:
-            mine = range(rank, nframes, world)
-            counters[row, 0] += dev(p, [(pi << 40) + f * frame_blocks for f in mine])
+            if len(mine):
+                counters[row, 0] += dev(p, (pi << 40) + mine.start * frame_blocks, len(mine) * frame_blocks)
             counters[row, 1] += len(mine) * frame_blocks * code.blen
             continue
-        for f in range(rank, nframes, world):
+        for f in mine:
             first = (pi << 40) + f * frame_blocks
             if channel == SOFT:
                 info, data = ch.awgn_blocks(code, frame_blocks, ch.noise_scaling(p), seed,

@@ -102,7 +102,35 @@ def test_viterbi_awgn_curve(torch_cuda, name):
     _run(curve, range(8), lambda k: max(8_000_000, 4 * _ref_bits(curve, k)), "viterbi")
 
 
-VITERBI_BSC = [c["name"] for c in PUB["curves"] if c["channel"] == "bsc" and c["decoder"] == "viterbi"]
+# results/binary_symmetric_channel.m:7 (code 1) disagrees with the reference's own sources: the
+# compiled, unmodified reference decoder + driver give a BER 2-4 % above the table at every point
+# (tests/golden/make_reference_ber.py: 0.1159 at p = 0.1 over 40 M bits vs 0.1126), as does this GPU
+# decoder -- that curve came from another build. Checked against the reference run instead
+# (test_viterbi_bsc_code1_vs_reference_run); the table comparison is kept as a strict xfail.
+PUBLISHED_MISMATCH = {"ber_coded_b": "results/binary_symmetric_channel.m:7 is 2-4 % below the compiled "
+                                     "reference's own BER (tests/golden/reference_ber.json)"}
+VITERBI_BSC = [pytest.param(c["name"], marks=pytest.mark.xfail(strict=True, reason=PUBLISHED_MISMATCH[c["name"]]))
+               if c["name"] in PUBLISHED_MISMATCH else c["name"]
+               for c in PUB["curves"] if c["channel"] == "bsc" and c["decoder"] == "viterbi"]
+REFRUN = json.load(open(os.path.join(REPO, "tests", "golden", "reference_ber.json")))["points"]
+
+
+def test_viterbi_bsc_code1_vs_reference_run(torch_cuda):
+    """Code 1 on the BSC against the compiled reference's own BER (same acceptance rule, the run's
+    bits in place of the table's schedule): 7 crossover probabilities, 40 M reference bits each."""
+    bad, out = [], []
+    for k, ref in enumerate(REFRUN):
+        code = CODEBOOK[ref["codebook_index"]]
+        (r,) = sim.ber_sweep(code, [ref["p_ppm"]], HARD, bits_per_point=lambda _p: 80_000_000,
+                             seed=0xC1 + k, device_channel=True, point_index=k)
+        q = (r.errors + ref["errors"]) / (r.bits + ref["bits"])
+        tol = Z * math.sqrt(code.blen * q * (1 - q) * (1.0 / r.bits + 1.0 / ref["bits"]))
+        msg = f"p={ref['p_ppm']}: {r.ber:.5g} vs reference run {ref['ber']:.5g} +- {tol:.3g}"
+        out.append(msg)
+        if abs(r.ber - ref["ber"]) > tol:
+            bad.append(msg)
+    print("\n".join(out))
+    assert not bad, "\n".join(bad)
 
 
 @pytest.mark.parametrize("name", VITERBI_BSC)

@@ -117,7 +117,7 @@ def _cli_worker(rank, world, port, outdir, paths):
 
 
 def test_sweep_cli_gloo_world2_matches_one_process(tmp_path, monkeypatch, capsys):
-    """`python -m ccviterbi.sim --gpus 2`: frames f = r, r + 2, ... per rank, one all-reduce of the
+    """`python -m ccviterbi.sim --gpus 2`: a contiguous frame range per rank, one all-reduce of the
     [points][errors, bits] table; the counts equal one process decoding every frame."""
     mp.spawn(_cli_worker, args=(2, launch.free_port(), str(tmp_path), [REPO, PKG_ROOT, os.path.join(REPO, "tests")]),
              nprocs=2, join=True)

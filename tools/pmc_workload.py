@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Summarise the three PMC passes of tools/pmc_workload.sh into per-launch figures of the workload's
+dominant kernel, merged into a JSON keyed like bench.py's workload_key_of() (copy it to
+profiles/pmc_workloads.json to have bench.py report traffic / traffic_frac / valu_frac).
+
+HBM bytes = FETCH_SIZE * 1024 * read_scale + WRITE_SIZE * 1024 * write_scale, the scales from a device
+copy of a known byte count profiled in the same run (MI355X_MICROARCH.md: FETCH_SIZE counts half of a
+wide streaming read on gfx950). SQ / GRBM counters are the device totals rocprofv3 reports per
+dispatch (GRBM_GUI_ACTIVE summed over the 8 XCDs). The kernel is the one with the largest total
+duration among the probe's dispatches (the decode).
+
+usage: pmc_workload.py PASS_DIR OUT_JSON [workload args...]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def counters(pass_dir):
+    """{kernel: {counter: [per-dispatch value]}}, {kernel: [duration ns]}"""
+    vals = defaultdict(lambda: defaultdict(float))
+    names = {}
+    for f in glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            d = r["Dispatch_Id"]
+            vals[d][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[d] = r["Kernel_Name"]
+    durs = defaultdict(list)
+    for f in glob.glob(os.path.join(pass_dir, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            durs[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    out = defaultdict(lambda: defaultdict(list))
+    for d, cs in vals.items():
+        for c, v in cs.items():
+            out[names[d]][c].append(v)
+    return out, durs
+
+
+def avg(xs):
+    return sum(xs) / len(xs) if xs else None
+
+
+def main():
+    root, out_json = sys.argv[1], sys.argv[2]
+    ap = argparse.ArgumentParser()
+    for a, d in (("--code", None), ("--frames", "104"), ("--layout", "block"), ("--channel", "awgn"),
+                 ("--decoder", "viterbi"), ("--ebn0", "4.0"), ("--p-ppm", "50000"), ("--reps", "3")):
+        ap.add_argument(a, default=d)
+    args = ap.parse_args(sys.argv[3:])
+    args.code = args.code or ("k7" if args.decoder == "viterbi" else "k15")
+    args.frames = int(args.frames)
+    import bench
+    key = bench.workload_key_of(args)
+    fetch, durs = counters(os.path.join(root, "FETCH"))
+    write, _ = counters(os.path.join(root, "WRITE"))
+    sq, sq_durs = counters(os.path.join(root, "SQ"))
+    copy_k = [k for k in fetch if "copy" in k.lower() or "elementwise" in k.lower()]
+    dec_k = max((k for k in durs if k not in copy_k), key=lambda k: sum(durs[k]))
+    log = open(os.path.join(root, "FETCH.log")).read().split()
+    copy_bytes = int(log[log.index("copy_bytes") + 1])
+    c_fetch = avg(fetch[copy_k[0]]["FETCH_SIZE"]) * 1024
+    c_write = avg(write[copy_k[0]]["WRITE_SIZE"]) * 1024
+    read_scale, write_scale = copy_bytes / c_fetch, copy_bytes / c_write
+    d_fetch = avg(fetch[dec_k]["FETCH_SIZE"]) * 1024
+    d_write = avg(write[dec_k]["WRITE_SIZE"]) * 1024
+    rec = {
+        "kernel": dec_k,
+        "launches_profiled": len(durs[dec_k]),
+        "kernel_ns": avg(sq_durs.get(dec_k, durs[dec_k])),
+        "hbm_bytes_per_launch": int(d_fetch * read_scale + d_write * write_scale),
+        "raw_fetch_bytes_per_launch": d_fetch, "raw_write_bytes_per_launch": d_write,
+        "calibration": {"copy_kernel": copy_k[0], "copy_bytes": copy_bytes, "read_scale": read_scale,
+                        "write_scale": write_scale},
+        "source": os.path.relpath(root),
+    }
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_BUSY_CYCLES",
+              "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"):
+        v = avg(sq[dec_k].get(c, []))
+        if v is not None:
+            rec[c.lower()] = v
+    if rec.get("sq_insts_valu") and rec.get("grbm_gui_active"):
+        rec["valu_frac"] = rec["sq_insts_valu"] / (512.0 * rec["grbm_gui_active"] / 8.0)
+        rec["clock_ghz"] = rec["grbm_gui_active"] / 8.0 / rec["kernel_ns"]
+    try:
+        doc = json.load(open(out_json))
+    except (OSError, ValueError):
+        doc = {}
+    doc[key] = rec
+    os.makedirs(os.path.dirname(os.path.abspath(out_json)), exist_ok=True)
+    with open(out_json, "w") as f:
+        json.dump(doc, f, indent=1, sort_keys=True)
+    print(key, json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
