@@ -60,6 +60,7 @@ def main():
     fetch, durs = counters(os.path.join(root, "FETCH"))
     write, _ = counters(os.path.join(root, "WRITE"))
     sq, sq_durs = counters(os.path.join(root, "SQ"))
+    stall, _ = counters(os.path.join(root, "STALL"))
     copy_k = [k for k in fetch if "copy" in k.lower() or "elementwise" in k.lower()]
     dec_k = max((k for k in durs if k not in copy_k), key=lambda k: sum(durs[k]))
     log = open(os.path.join(root, "FETCH.log")).read().split()
@@ -84,6 +85,19 @@ def main():
         v = avg(sq[dec_k].get(c, []))
         if v is not None:
             rec[c.lower()] = v
+    st = {}
+    for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_LDS",
+              "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_SCA", "SQ_WAVE_CYCLES"):
+        v = avg(stall.get(dec_k, {}).get(c, []))
+        if v is not None:
+            st[c.lower()] = v
+    if st.get("sq_wave_cycles"):
+        # disjoint split of wave lifetime (MI355X_MICROARCH.md PMC table): parked on s_waitcnt /
+        # barrier, issue-stalled, issuing
+        for c in ("sq_wait_any", "sq_wait_inst_any", "sq_active_inst_any"):
+            if c in st:
+                st[c + "_frac"] = st[c] / st["sq_wave_cycles"]
+        rec["stall"] = st
     if rec.get("sq_insts_valu") and rec.get("grbm_gui_active"):
         rec["valu_frac"] = rec["sq_insts_valu"] / (512.0 * rec["grbm_gui_active"] / 8.0)
         rec["clock_ghz"] = rec["grbm_gui_active"] / 8.0 / rec["kernel_ns"]

@@ -2,7 +2,7 @@
 # PMC figures of one bench workload's dominant kernel, three rocprofv3 passes (one counter group
 # each, kernel trace only -- gfx950 cannot hold FETCH_SIZE and WRITE_SIZE in one pass):
 #   FETCH_SIZE | WRITE_SIZE | SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES
-#                             SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU + GRBM_GUI_ACTIVE
+#                             SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU + GRBM_GUI_ACTIVE | stall split
 # over tools/traffic_probe.py (a calibration copy + the bench decode), then tools/pmc_workload.py
 # merges the per-launch figures into gpurun_out/pmc/pmc_workloads.json under the bench's workload key.
 # Usage: tools/pmc_workload.sh [traffic_probe / bench.py workload args...]
@@ -21,4 +21,5 @@ pass() {
 pass FETCH FETCH_SIZE
 pass WRITE WRITE_SIZE
 pass SQ SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
+pass STALL SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES
 python tools/pmc_workload.py $OUT gpurun_out/pmc/pmc_workloads.json $ARGS
