@@ -18,6 +18,7 @@
 #include "trellis.hpp"
 
 namespace ccv {
+constexpr size_t kHostLatencyMaxBlocks = 64;   // ccv_decode_host batches decoded by the generic kernel
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s);   // stack.hip
 bool stack_rows_eligible(int n, int K, int T);                           // stack.hip
 bool stack_symtab_eligible(int n, int K, int T);                         // stack.hip
@@ -71,6 +72,32 @@ struct DeviceBuffer {
   }
 };
 
+// Page-locked host memory the device reads and writes directly (zero-copy): the streaming decode
+// path's per-plan staging, so a single block costs one kernel launch and one synchronise.
+struct PinnedBuffer {
+  void* host = nullptr;
+  void* dev = nullptr;
+  size_t bytes = 0;
+  int grow(size_t need, hipStream_t sync_stream) {
+    if (need <= bytes) return 0;
+    if (host) {
+      HIP_TRY(hipStreamSynchronize(sync_stream));
+      HIP_TRY(hipHostFree(host));
+      host = dev = nullptr;
+      bytes = 0;
+    }
+    HIP_TRY(hipHostMalloc(&host, need, hipHostMallocDefault));
+    HIP_TRY(hipHostGetDevicePointer(&dev, host, 0));
+    bytes = need;
+    return 0;
+  }
+  void release() {
+    if (host) (void)hipHostFree(host);
+    host = dev = nullptr;
+    bytes = 0;
+  }
+};
+
 }  // namespace
 
 struct ccv_plan {
@@ -95,6 +122,8 @@ struct ccv_plan {
   uint8_t* d_exp = nullptr;          // device copy of exp (generic kernel)
   DeviceBuffer dec;                  // register-kernel decision scratch
   DeviceBuffer host_in, host_out, host_pm;   // staging for ccv_decode_host
+  PinnedBuffer lat_in, lat_out, lat_pm;        // zero-copy staging of small ccv_decode_host calls
+  bool generic_ok = false;                     // the generic kernel can run this code (d_exp built)
   DeviceBuffer sim_info, sim_out;             // ccv_simulate_device scratch (caller passed none)
   hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
 };
@@ -260,20 +289,26 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
     p->d.decision_word_bytes = 8;
     p->d.lanes = 1 << (K - 7);
   } else {
-    const int S = p->d.states;
     p->d.kernel = CCV_KERNEL_GENERIC;
+  }
+  // The generic kernel (one workgroup per block) also serves small host batches of the register
+  // codes: it decodes a block in a few microseconds, where one register-trellis lane takes ~17 us.
+  {
+    const int S = p->d.states;
     p->generic_spt = S <= ccv::kGenericMaxThreads ? 1 : S / ccv::kGenericMaxThreads;
     p->generic_threads = S <= 64 ? 64 : (S <= ccv::kGenericMaxThreads ? S : ccv::kGenericMaxThreads);
     const int NS = 1 << n;
     p->generic_chunk = 4096 / NS < 1 ? 1 : 4096 / NS;
     if (p->generic_chunk > p->d.steps) p->generic_chunk = p->d.steps;
     p->generic_lds = ccv::generic_lds_bytes(n, K, p->d.steps, p->generic_chunk, channel == CCV_HARD);
-    if (p->generic_lds > 160 * 1024) {
+    p->generic_ok = p->generic_lds <= 160 * 1024 && p->generic_spt <= 8;
+    if (p->d.kernel == CCV_KERNEL_GENERIC && !p->generic_ok) {
       delete p;
       return fail("code needs %zu B of LDS per block", p->generic_lds);
     }
-    if (hipMalloc(&p->d_exp, p->exp.size()) != hipSuccess ||
-        hipMemcpy(p->d_exp, p->exp.data(), p->exp.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    if (p->generic_ok &&
+        (hipMalloc(&p->d_exp, p->exp.size()) != hipSuccess ||
+         hipMemcpy(p->d_exp, p->exp.data(), p->exp.size(), hipMemcpyHostToDevice) != hipSuccess)) {
       (void)hipGetLastError();
       if (p->d_exp) (void)hipFree(p->d_exp);
       delete p;
@@ -297,6 +332,9 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->host_in.release();
   p->host_out.release();
   p->host_pm.release();
+  p->lat_in.release();
+  p->lat_out.release();
+  p->lat_pm.release();
   p->sim_info.release();
   p->sim_out.release();
   p->counter.release();
@@ -739,11 +777,48 @@ int ccv_stack_decode_host(ccv_plan* p, const void* in, size_t nblocks, const voi
   return 0;
 }
 
+// Small host batches (the streaming decoder_input path completes one block per call): the input is
+// copied into page-locked memory the kernel reads directly, the generic kernel (one workgroup per
+// block, a few microseconds) writes the output and path metrics straight into page-locked memory, and
+// one synchronise ends the call -- no device allocation, no DMA copies. CCV_HOST_LATENCY=0 turns it
+// off (A/B).
+static int decode_host_latency(ccv_plan* p, const void* in, size_t nblocks, uint8_t* out,
+                               int32_t* path_metric) {
+  const bool hard = p->d.channel == CCV_HARD;
+  const size_t in_bytes = nblocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes;
+  const size_t out_bytes = nblocks * (size_t)p->d.out_bytes;
+  if (p->lat_in.grow(in_bytes, p->stream) || p->lat_out.grow(out_bytes, p->stream) ||
+      p->lat_pm.grow(nblocks * sizeof(int32_t), p->stream))
+    return -1;
+  memcpy(p->lat_in.host, in, in_bytes);
+  ccv::GenericArgs a{};
+  a.in = p->lat_in.dev;
+  a.exp = p->d_exp;
+  a.n = p->d.n;
+  a.K = p->d.K;
+  a.T = p->d.steps;
+  a.blen = p->d.blen;
+  a.nblocks = (int)nblocks;
+  a.chunk = p->generic_chunk;
+  a.out = static_cast<uint8_t*>(p->lat_out.dev);
+  a.path_metric = hard ? static_cast<int32_t*>(p->lat_pm.dev) : nullptr;
+  HIP_TRY(hard ? launch_generic<true>(a, *p, nblocks, p->stream)
+               : launch_generic<false>(a, *p, nblocks, p->stream));
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  memcpy(out, p->lat_out.host, out_bytes);
+  if (hard && path_metric) memcpy(path_metric, p->lat_pm.host, nblocks * sizeof(int32_t));
+  return 0;
+}
+
 int ccv_decode_host(ccv_plan* p, const void* in, size_t nblocks, uint8_t* out, int32_t* path_metric) {
   if (!p) return fail("null plan");
   if (p->step_major) return fail("ccv_decode_host takes block-major input");
   if (nblocks == 0) return 0;
   if (!in || !out) return fail("null host buffer");
+  if (nblocks <= ccv::kHostLatencyMaxBlocks && p->generic_ok && !p->stack && !p->fano) {
+    const char* env = std::getenv("CCV_HOST_LATENCY");
+    if (!env || env[0] != '0') return decode_host_latency(p, in, nblocks, out, path_metric);
+  }
   const size_t in_bytes = nblocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes;
   const size_t out_bytes = nblocks * (size_t)p->d.out_bytes;
   const bool want_pm = p->d.channel == CCV_HARD && path_metric;

@@ -20,6 +20,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "code.h"
 #include "codebook.h"
@@ -48,6 +49,23 @@ typedef struct {
     FILE *f_rx, *f_out, *f_pm;
 } harness_t;
 
+/* wall time spent inside decoder_input() (the decoder, and the output callback it calls) */
+static double g_decoder_seconds = 0.0;
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+static void timed_decoder_input(struct decoder* d, void* data, uint8_t len) {
+    double t0 = now_s();
+#ifdef HARNESS_AWGN
+    (void)decoder_input(d, (float*)data, len);
+#else
+    (void)decoder_input(d, (uint8_t*)data, len);
+#endif
+    g_decoder_seconds += now_s() - t0;
+}
+
 static size_t steps_of(const struct code_param* p) { return (size_t)p->block_len + p->constr_len - 1; }
 
 static void count_errors(harness_t* h, const uint8_t* data, uint8_t len) {
@@ -73,7 +91,7 @@ static int on_mapped(float* data, uint8_t len, void* ud) {
 static int on_demapped(float* data, uint8_t len, void* ud) {
     harness_t* h = (harness_t*)ud;
     fwrite(data, sizeof(float), len, h->f_rx);
-    (void)decoder_input(h->decoder, data, len);
+    timed_decoder_input(h->decoder, data, len);
     return -1;
 }
 static int on_decoded(uint8_t* data, uint8_t len, void* ud) {
@@ -90,7 +108,7 @@ static int on_encoded(uint8_t* data, uint8_t len, void* ud) {
         for (uint8_t k = 0; k < h->param.symlen_out; ++k)
             if ((rand() % 1000000) < h->p_ppm) data[i] ^= (uint8_t)(1 << k);
     fwrite(data, 1, len, h->f_rx);
-    (void)decoder_input(h->decoder, data, len);
+    timed_decoder_input(h->decoder, data, len);
     return -1;
 }
 static int on_decoded(uint8_t* data, uint8_t len, int32_t path_metric, void* ud) {
@@ -180,6 +198,7 @@ int main(int argc, char** argv) {
 #ifndef HARNESS_AWGN
     h.f_pm = open_out(prefix, "pm");
 #endif
+    double t_start = now_s();
     srand(seed);
     size_t ib = ((size_t)h.param.block_len + 7) / 8;
     for (long k = 0; k < nblocks; ++k) {
@@ -187,6 +206,7 @@ int main(int argc, char** argv) {
         fwrite(h.info, 1, ib, f_info);
         (void)encoder_input(h.encoder, h.info, h.param.block_len);
     }
+    double wall = now_s() - t_start;
     fclose(f_info);
     fclose(h.f_rx);
     fclose(h.f_out);
@@ -203,6 +223,7 @@ int main(int argc, char** argv) {
             h.param.fano_bit_metrics ? h.param.fano_bit_metrics[1] : 0);
     fprintf(meta, "bit_metric0 %d\nbit_metric1 %d\n", h.param.bit_metrics ? h.param.bit_metrics[0] : 0,
             h.param.bit_metrics ? h.param.bit_metrics[1] : 0);
+    fprintf(meta, "decoder_seconds %.6f\nwall_seconds %.6f\n", g_decoder_seconds, wall);
     fclose(meta);
     return h.block == (size_t)nblocks ? 0 : 1;
 }
