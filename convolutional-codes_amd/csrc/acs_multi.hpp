@@ -32,18 +32,41 @@
 
 namespace ccv {
 
-template <CodeSpec C>
+// Physical layout: lane bit b of a block's lane group sits at physical state bit LB<b> (LB1 unused
+// for K = 8), the 6 register bits at the remaining positions in increasing order. The default puts
+// the lanes on the top bits (phys = q << 6 | r): the cross-lane phases are the last K - 7 of each
+// period. LB = {0, 3} (the persistent K = 9 kernel) moves them to phases 0 and 3, which keeps more
+// equal-candidate ("twin") states of the x86-idiom trellis inside one lane (tools/
+// trellis_value_numbering.py: 100.5 adds / 50.3 mins per lane-step instead of 105.3 / 52.6).
+template <CodeSpec C, int LB0 = 6, int LB1 = 7>
 struct Multi {
   static constexpr int n = C.K - 1;          // state bits
   static constexpr int QB = C.K - 7;         // lane bits
   static constexpr int L = 1 << QB;          // lanes per block
   static constexpr int S = 1 << n;
   static constexpr int NS = 1 << C.n;
+  static_assert(QB == 1 || LB0 != LB1, "distinct lane bits");
+  static constexpr bool is_lane(int P) { return P == LB0 || (QB == 2 && P == LB1); }
+  static constexpr int lane_of(int P) { return P == LB0 ? 0 : 1; }      // which q bit phys bit P is
+  static constexpr int reg_bit(int P) {                                 // which r bit phys bit P is
+    int k = 0;
+    for (int b = 0; b < P; ++b) k += is_lane(b) ? 0 : 1;
+    return k;
+  }
+  static constexpr uint32_t phys(int q, int r) {
+    uint32_t x = 0;
+    int k = 0;
+    for (int b = 0; b < n; ++b) {
+      if (is_lane(b)) x |= (uint32_t)((q >> lane_of(b)) & 1) << b;
+      else x |= (uint32_t)((r >> k++) & 1) << b;
+    }
+    return x;
+  }
   static constexpr uint32_t rotr(uint32_t x, int p) {
     p %= n;
     return p == 0 ? x : (((x >> p) | (x << (n - p))) & (S - 1));
   }
-  static constexpr uint32_t logical(int q, int r, int p) { return rotr(((uint32_t)q << 6) | (uint32_t)r, p); }
+  static constexpr uint32_t logical(int q, int r, int p) { return rotr(phys(q, r), p); }
 };
 
 __device__ __forceinline__ uint32_t rotl_bits(uint32_t x, int k, int n) {
@@ -71,13 +94,16 @@ __device__ __forceinline__ MT select_bm(const MT (&BM)[NS], bool qb0, bool qb1) 
   }
 }
 
+// quad_perm moves with every lane enabled: no "old" value is ever kept, so bound_ctrl and the
+// old-operand-free form let the compiler fuse the move into its consumer or skip the v_mov 0
+// that an update_dpp(0, ...) needs.
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL, typename MT>
 __device__ __forceinline__ MT dpp(MT x) {
@@ -89,18 +115,18 @@ __device__ __forceinline__ MT dpp(MT x) {
 // In-lane phase P: butterfly (R, R | 1 << P); the i = 0 survivor's decision is shifted into `lo`,
 // the i = 1 survivor's into `hi`, so bit compress_P(R) of lo / hi belongs to register R / R | 1 << P.
 // Cross phase: the decision of register R goes to bit R of (hi:lo).
-template <CodeSpec C, int P, int R, bool SAT, typename MT>
+template <CodeSpec C, int P, int R, bool SAT, typename MT, class X = Multi<C>>
 __device__ __forceinline__ void multi_acs(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0, bool qb1,
                                           uint32_t& lo, uint32_t& hi) {
-  using X = Multi<C>;
   constexpr int L = X::L;
   auto sat = [](MT v) {
     if constexpr (SAT) return vmin(v, (MT)0xFF00);   // binary-symmetric-channel/viterbi-decoder.c:127-130
     else return v;
   };
-  if constexpr (P < 6) {
-    if constexpr ((R & (1 << P)) == 0) {
-      constexpr int R1 = R | (1 << P);
+  if constexpr (!X::is_lane(P)) {
+    constexpr int k = X::reg_bit(P);
+    if constexpr ((R & (1 << k)) == 0) {
+      constexpr int R1 = R | (1 << k);
       constexpr auto e = [](int q, int odd, int in) {
         return expected_symbol(C, X::logical(q, R, P) | (uint32_t)odd, in);
       };
@@ -116,7 +142,7 @@ __device__ __forceinline__ void multi_acs(MT (&M)[64], const MT (&BM)[1 << C.n],
   } else {
     // cross-lane butterfly on lane bit B: even predecessor in the lane with bit B clear, odd in the
     // lane with it set, same register; this lane's new state has input bit = its own bit B
-    constexpr int B = P - 6;
+    constexpr int B = X::lane_of(P);
     constexpr int CE = B == 0 ? 0xA0 : 0x44;   // quad_perm [0,0,2,2] / [0,1,0,1]
     constexpr int CO = B == 0 ? 0xF5 : 0xEE;   // quad_perm [1,1,3,3] / [2,3,2,3]
     constexpr auto e = [](int q, int odd) {
@@ -137,24 +163,24 @@ __device__ __forceinline__ void multi_acs(MT (&M)[64], const MT (&BM)[1 << C.n],
 // unreachable (its candidate is +inf / saturated 0xFF00 and never wins the strict compare), so each
 // new state is its even predecessor plus the branch metric and its decision is 0 -- the adds only
 // (see acs_persist.hpp growth_step; unreachable states stay +inf / 0xFF00 exactly).
-template <CodeSpec C, int P, int R, bool SAT, typename MT>
+template <CodeSpec C, int P, int R, bool SAT, typename MT, class X = Multi<C>>
 __device__ __forceinline__ void multi_growth(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0, bool qb1) {
-  using X = Multi<C>;
   constexpr int L = X::L;
   auto sat = [](MT v) {
     if constexpr (SAT) return vmin(v, (MT)0xFF00);   // binary-symmetric-channel/viterbi-decoder.c:127-130
     else return v;
   };
-  if constexpr (P < 6) {
-    if constexpr ((R & (1 << P)) == 0) {
-      constexpr int R1 = R | (1 << P);
+  if constexpr (!X::is_lane(P)) {
+    constexpr int k = X::reg_bit(P);
+    if constexpr ((R & (1 << k)) == 0) {
+      constexpr int R1 = R | (1 << k);
       constexpr auto e = [](int q, int in) { return expected_symbol(C, X::logical(q, R, P), in); };
       const MT even = M[R];
       M[R] = sat(even + select_bm<L, e(0, 0), e(1 % L, 0), e(2 % L, 0), e(3 % L, 0)>(BM, qb0, qb1));
       M[R1] = sat(even + select_bm<L, e(0, 1), e(1 % L, 1), e(2 % L, 1), e(3 % L, 1)>(BM, qb0, qb1));
     }
   } else {
-    constexpr int B = P - 6;
+    constexpr int B = X::lane_of(P);
     constexpr int CE = B == 0 ? 0xA0 : 0x44;   // quad_perm [0,0,2,2] / [0,1,0,1]
     constexpr auto e = [](int q) {
       const int qe = q & ~(1 << B);
@@ -164,30 +190,37 @@ __device__ __forceinline__ void multi_growth(MT (&M)[64], const MT (&BM)[1 << C.
   }
 }
 
-template <CodeSpec C, int P, bool SAT, typename MT, size_t... I>
+template <CodeSpec C, int P, bool SAT, typename MT, class X = Multi<C>, size_t... I>
 __device__ __forceinline__ void multi_growth_step_impl(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0,
                                                        bool qb1, std::index_sequence<I...>) {
-  (multi_growth<C, P, 63 - (int)I, SAT, MT>(M, BM, qb0, qb1), ...);
+  (multi_growth<C, P, 63 - (int)I, SAT, MT, X>(M, BM, qb0, qb1), ...);
 }
 
-template <CodeSpec C, int P, bool SAT, typename MT, size_t... I>
+template <CodeSpec C, int P, bool SAT, typename MT, class X = Multi<C>, size_t... I>
 __device__ __forceinline__ uint64_t multi_step_impl(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0,
                                                     bool qb1, std::index_sequence<I...>) {
   uint32_t lo = 0, hi = 0;
-  (multi_acs<C, P, 63 - (int)I, SAT, MT>(M, BM, qb0, qb1, lo, hi), ...);   // descending registers
+  (multi_acs<C, P, 63 - (int)I, SAT, MT, X>(M, BM, qb0, qb1, lo, hi), ...);   // descending registers
   return ((uint64_t)hi << 32) | lo;
 }
 
-template <CodeSpec C, int P, bool SAT, typename MT>
+template <CodeSpec C, int P, bool SAT, typename MT, class X = Multi<C>>
 __device__ __forceinline__ uint64_t multi_step(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0, bool qb1) {
-  return multi_step_impl<C, P, SAT, MT>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
+  return multi_step_impl<C, P, SAT, MT, X>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
 }
 
-// Bit of register r's decision in the word stored at phase p (see multi_acs).
+// Bit of register r's decision in the word stored at an in-lane phase that pairs on register bit k
+// (see multi_acs: bit 5 = r's bit k, below it the other five bits in order); a cross phase stores
+// register r's decision at bit r.
+__device__ __forceinline__ uint32_t multi_dec_pos_k(uint32_t r, int k) {
+  const uint32_t low = r & ((1u << k) - 1u);
+  return (((r >> k) & 1u) << 5) | ((r >> (k + 1)) << k) | low;
+}
+// The same for the default layout (lanes on the top physical bits): phase p < 6 pairs on register
+// bit p.
 __device__ __forceinline__ uint32_t multi_dec_pos(uint32_t r, int p) {
   if (p >= 6) return r;
-  const uint32_t low = r & ((1u << p) - 1u);
-  return (((r >> p) & 1u) << 5) | ((r >> (p + 1)) << p) | low;
+  return multi_dec_pos_k(r, p);
 }
 
 // One period (phases 0..n-1) of steps t .. t+n-1, each guarded by t + P < T; slot P of the input
@@ -240,10 +273,22 @@ __device__ __forceinline__ uint32_t multi_argmin(const MT (&M)[64], int phase, i
 // compare/select chain (acs_reg.hpp argmin_state): the logical index is (q << 6) | r, so the answer
 // is the lowest lane holding the group's minimum and, in it, the lowest register. v_min3 tree,
 // lane minimum, "differs" mask from the sign of min - M[r], lowest clear bit, lane minimum.
-template <CodeSpec C>
+// Physical state of (lane q, register r) at run time (Multi::phys).
+template <class X>
+__device__ __forceinline__ uint32_t multi_phys(uint32_t q, uint32_t r) {
+  uint32_t x = 0;
+  int k = 0;
+#pragma unroll
+  for (int b = 0; b < X::n; ++b) {
+    if (X::is_lane(b)) x |= ((q >> X::lane_of(b)) & 1u) << b;
+    else x |= ((r >> k++) & 1u) << b;
+  }
+  return x;
+}
+
+template <CodeSpec C, class X = Multi<C>>
 __device__ __forceinline__ uint32_t multi_argmin_phase0(const float (&M)[64], int q, float sentinel,
                                                         float& best) {
-  using X = Multi<C>;
   float mn = tree_min<64, float>(M);
 #pragma unroll
   for (int off = 1; off < X::L; off <<= 1) mn = vmin(mn, __shfl_xor(mn, off, 64));
@@ -254,7 +299,9 @@ __device__ __forceinline__ uint32_t multi_argmin_phase0(const float (&M)[64], in
     hi = __builtin_amdgcn_alignbit(hi, min_minus(mn, M[r + 32]), 31);
   }
   const uint64_t eq = ~(((uint64_t)hi << 32) | lo);
-  uint32_t idx = eq ? (((uint32_t)q << 6) | (uint32_t)__builtin_ctzll(eq)) : 0xFFFFFFFFu;
+  // registers map to physical bits in increasing order: the lowest register is the lowest state of
+  // the lane; across lanes the lowest physical (= logical, phase 0) index wins
+  uint32_t idx = eq ? multi_phys<X>((uint32_t)q, (uint32_t)__builtin_ctzll(eq)) : 0xFFFFFFFFu;
 #pragma unroll
   for (int off = 1; off < X::L; off <<= 1) {
     const uint32_t o = (uint32_t)__shfl_xor((int)idx, off, 64);
@@ -491,10 +538,15 @@ void viterbi_multi_regdec(RegArgs a) {
 // period 0 is the growth from the reset metrics (adds only, no decisions); the 40 main steps keep
 // their decision words in VGPRs; the input is staged by LDS-DMA one chunk ahead (2 KiB per chunk:
 // 16 blocks x 8 steps x 16 bytes; the 4 lanes of a block read the same row).
-template <CodeSpec C, int BLEN>
-__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
+// Ablation switches for timing studies (tools/k9_bench.hip); production kernels use 0.
+enum : int { kMultiNoTraceback = 1, kMultiNoMem = 2, kMultiBpermuteTraceback = 4 };
+
+// LDSP: main periods whose decision words go to LDS instead of VGPRs (8 x 8 B x 64 lanes = 4 KiB
+// per period per wave): each one frees 16 VGPRs, and with two of them the kernel fits 3 waves per SIMD.
+template <CodeSpec C, int BLEN, int ABLATE = 0, int LDSP = 0, int LB0 = 6, int LB1 = 7>
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(LDSP >= 2 ? 3 : 2)))
 void viterbi_multi_persist(RegArgs a, int ngroups) {
-  using X = Multi<C>;
+  using X = Multi<C, LB0, LB1>;
   using MT = float;
   static_assert(C.K == 9 && C.n == 2, "K = 9, r = 1/2: the period (8 steps) is the 8-step chunk");
   constexpr int n = X::n;                     // 8 phases per period
@@ -514,9 +566,11 @@ void viterbi_multi_persist(RegArgs a, int ngroups) {
   const int nb = a.nblocks;
   const int stride_groups = gridDim.x;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[BUF];
+  __shared__ uint64_t ldsdec[LDSP > 0 ? LDSP * n * kRegThreads : 1];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   // DMA k of a chunk: unit k*64 + lane = block r (of 16), 16-byte step j of its chunk
   auto issue_chunk = [&](int g, int c) __attribute__((always_inline)) {
+    if constexpr ((ABLATE & kMultiNoMem) != 0) return;
 #pragma unroll
     for (int k = 0; k < UNITS / kRegThreads; ++k) {
       const int unit = k * kRegThreads + lane;
@@ -540,11 +594,21 @@ void viterbi_multi_persist(RegArgs a, int ngroups) {
     MT M[64];
 #pragma unroll
     for (int r = 0; r < 64; ++r) M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
-    uint64_t D[NMAIN][n];
+    uint64_t D[NMAIN - LDSP > 0 ? NMAIN - LDSP : 1][n];
     uint8_t info[IB];
     auto period_at = [&]<int p>() __attribute__((always_inline)) {
       f32x4 chunk[n];
       wait_vmcnt<0>();
+      if constexpr ((ABLATE & kMultiNoMem) != 0) {   // full-entropy synthetic rows in [1, 2)
+        uint32_t ln = (uint32_t)(lane / X::L + g * 131 + p * 977) * 0x9E3779B9u;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int x = 0; x < n; ++x) {
+          const uint32_t r0 = ln ^ (uint32_t)(x * 0x85EBCA6Bu), r1 = r0 * 0xC2B2AE35u;
+          chunk[x] = f32x4{__uint_as_float((r0 >> 9) | 0x3F800000u), __uint_as_float((r1 >> 9) | 0x3F800000u),
+                           __uint_as_float((r0 & 0x7FFFFFu) | 0x3F800000u), __uint_as_float((r1 & 0x7FFFFFu) | 0x3F800000u)};
+        }
+      } else
       [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
         ((chunk[xs] = lds_read_b128<xs * 16>(row)), ...);
       }(std::make_integer_sequence<int, n>{});
@@ -564,10 +628,14 @@ void viterbi_multi_persist(RegArgs a, int ngroups) {
       auto phase_at = [&]<int P>() __attribute__((always_inline)) {
         const MT BM[4] = {chunk[P].x, chunk[P].y, chunk[P].z, chunk[P].w};
         if constexpr (p == 0) {
-          multi_growth_step_impl<C, P, false, MT>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
+          multi_growth_step_impl<C, P, false, MT, X>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
         } else {
-          D[p - 1][P] = multi_step<C, P, false, MT>(M, BM, qb0, qb1);
-          pin(D[p - 1][P]);
+          if constexpr (p - 1 < LDSP) {
+            ldsdec[((p - 1) * n + P) * kRegThreads + lane] = multi_step<C, P, false, MT, X>(M, BM, qb0, qb1);
+          } else {
+            D[p - 1 - LDSP][P] = multi_step<C, P, false, MT, X>(M, BM, qb0, qb1);
+            pin(D[p - 1 - LDSP][P]);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       };
@@ -579,33 +647,105 @@ void viterbi_multi_persist(RegArgs a, int ngroups) {
       (period_at.template operator()<ps>(), ...);
     }(std::make_integer_sequence<int, NPER>{});
 
+    if constexpr ((ABLATE & kMultiNoTraceback) != 0) {
+      uint64_t x = 0;
+#pragma unroll
+      for (int pp = 0; pp < NMAIN - LDSP; ++pp)
+#pragma unroll
+        for (int P = 0; P < n; ++P) x ^= D[pp][P];
+#pragma unroll
+      for (int k = 0; k < LDSP * n; ++k) x ^= ldsdec[k * kRegThreads + lane];
+#pragma unroll
+      for (int r = 0; r < 64; ++r) x += __float_as_uint(M[r]);
+      if (blk < nb) reinterpret_cast<uint64_t*>(a.out)[blk * X::L + q] = x;
+      continue;
+    }
     MT best;
     static_assert(T % n == 0, "the persistent trellis ends on phase 0");
-    uint32_t st = multi_argmin_phase0<C>(M, q, __builtin_inff(), best);
+    uint32_t st = multi_argmin_phase0<C, X>(M, q, __builtin_inff(), best);
     uint64_t bits = 0;
-    auto back_step = [&]<int p, int P>() __attribute__((always_inline)) {
-      // survivors of step t sit at the phase-(t+1) positions (t mod n = P)
-      const uint32_t phys = rotl_bits(st, P + 1 == n ? 0 : P + 1, n);
-      uint32_t bit = 0;
-      if constexpr (p > 0) {
-        const uint32_t pos = multi_dec_pos(phys & 63u, P);
-        const uint64_t w = D[p - 1][P];
-        const uint32_t half = pos < 32 ? (uint32_t)w : (uint32_t)(w >> 32);
-        const int src = (gbase + (int)(phys >> 6)) << 2;
-        const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)half);
-        bit = (word >> (pos & 31)) & 1u;
+    if constexpr ((ABLATE & kMultiBpermuteTraceback) != 0) {   // round-2 traceback (A/B)
+      static_assert(LB0 == 6 && LB1 == 7, "the round-2 traceback knows the default layout only");
+      auto back_step = [&]<int p, int P>() __attribute__((always_inline)) {
+        // survivors of step t sit at the phase-(t+1) positions (t mod n = P)
+        const uint32_t phys = rotl_bits(st, P + 1 == n ? 0 : P + 1, n);
+        uint32_t bit = 0;
+        if constexpr (p > 0) {
+          const uint32_t pos = multi_dec_pos(phys & 63u, P);
+          const uint64_t w = p - 1 < LDSP ? ldsdec[((p - 1) * n + P) * kRegThreads + lane]
+                                          : D[p - 1 - LDSP < 0 ? 0 : p - 1 - LDSP][P];
+          const uint32_t half = pos < 32 ? (uint32_t)w : (uint32_t)(w >> 32);
+          const int src = (gbase + (int)(phys >> 6)) << 2;
+          const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)half);
+          bit = (word >> (pos & 31)) & 1u;
+        }
+        bits = (bits >> 1) | ((uint64_t)(st >> (C.K - 2)) << 63);
+        st = ((st << 1) & (X::S - 1)) | bit;
+      };
+      auto back_period = [&]<int p>() __attribute__((always_inline)) {
+        [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
+          (back_step.template operator()<p, n - 1 - Ps>(), ...);
+        }(std::make_integer_sequence<int, n>{});
+      };
+      [&]<int... ps>(std::integer_sequence<int, ps...>) __attribute__((always_inline)) {
+        (back_period.template operator()<NPER - 1 - ps>(), ...);
+      }(std::make_integer_sequence<int, NPER>{});
+    } else {
+      // Traceback in physical coordinates, no LDS round trip. The in-place ACS stores the survivor
+      // of logical state s at phase P+1 in physical slot rotl(s, P+1); one step back the logical
+      // state becomes ((s << 1) | d) mod S, whose physical slot at phase P is the same slot with
+      // ONLY bit P replaced by the decision d. So the walk keeps phys (8 bits: lane q = phys >> 6,
+      // register r = phys & 63), reads d at bit dec_pos(r, P) of lane q's word and writes it into
+      // bit P. The four lanes of a group hold the same phys: each extracts its own candidate bit
+      // and two quad DPP ORs give every lane all four, from which it takes lane q's.
+      // The decoded bits: the final state's 8 bits are the outputs of the last 8 steps, and the
+      // decision read at step t is the output of step t - 8 (it reaches the top state bit 8 steps
+      // earlier), so the history h = st, then (h << 1) | d per main step, holds output i at bit i.
+      // phase 0: physical = logical; the walk keeps phys split into its lane and register parts
+      uint32_t ql = 0, rl = 0;
+      {
+        int k = 0;
+#pragma unroll
+        for (int b = 0; b < n; ++b) {
+          if (X::is_lane(b)) ql |= ((st >> b) & 1u) << X::lane_of(b);
+          else rl |= ((st >> b) & 1u) << k++;
+        }
       }
-      bits = (bits >> 1) | ((uint64_t)(st >> (C.K - 2)) << 63);
-      st = ((st << 1) & (X::S - 1)) | bit;
-    };
-    auto back_period = [&]<int p>() __attribute__((always_inline)) {
-      [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
-        (back_step.template operator()<p, n - 1 - Ps>(), ...);
-      }(std::make_integer_sequence<int, n>{});
-    };
-    [&]<int... ps>(std::integer_sequence<int, ps...>) __attribute__((always_inline)) {
-      (back_period.template operator()<NPER - 1 - ps>(), ...);
-    }(std::make_integer_sequence<int, NPER>{});
+      uint64_t h = st;
+      const uint32_t qself = (uint32_t)q;
+      auto back_step = [&]<int p, int P>() __attribute__((always_inline)) {
+        if constexpr (p > 0) {
+          uint32_t pos;
+          if constexpr (X::is_lane(P)) pos = rl;
+          else pos = multi_dec_pos_k(rl, X::reg_bit(P));
+          uint64_t w;
+          if constexpr (p - 1 < LDSP) w = ldsdec[((p - 1) * n + P) * kRegThreads + lane];
+          else w = D[p - 1 - LDSP][P];
+          const uint32_t own = (uint32_t)(w >> pos) & 1u;
+          uint32_t m = own << qself;
+          m |= dpp_u32<0xB1>(m);   // quad_perm [1,0,3,2]
+          m |= dpp_u32<0x4E>(m);   // quad_perm [2,3,0,1]
+          const uint32_t d = (m >> ql) & 1u;
+          if constexpr (X::is_lane(P)) {
+            constexpr uint32_t bit = 1u << X::lane_of(P);
+            ql = (ql & ~bit) | (d << X::lane_of(P));
+          } else {
+            constexpr uint32_t bit = 1u << X::reg_bit(P);
+            rl = (rl & ~bit) | (d << X::reg_bit(P));
+          }
+          h = (h << 1) | d;
+        }
+      };
+      auto back_period = [&]<int p>() __attribute__((always_inline)) {
+        [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
+          (back_step.template operator()<p, n - 1 - Ps>(), ...);
+        }(std::make_integer_sequence<int, n>{});
+      };
+      [&]<int... ps>(std::integer_sequence<int, ps...>) __attribute__((always_inline)) {
+        (back_period.template operator()<NPER - 1 - ps>(), ...);
+      }(std::make_integer_sequence<int, NPER>{});
+      bits = __builtin_bitreverse64(h);   // bit 63 - t = output of step t
+    }
     if (q == 0 && blk < nb) {
       uint8_t* o = a.out + (size_t)blk * OB;
 #pragma unroll

@@ -35,9 +35,13 @@ using DecWord = typename std::conditional<(S > 32), uint64_t, uint32_t>::type;
 // fp32 min without the IEEE-mode canonicalisation (v_max x,x) hipcc inserts around fminf. Inputs
 // are always results of v_add_f32 (or +inf), so no signalling NaN can reach it.
 __device__ __forceinline__ float vmin(float a, float b) {
+#ifdef CCV_VMIN_BUILTIN
+  return __builtin_fminf(a, b);
+#else
   float r;
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
+#endif
 }
 __device__ __forceinline__ uint32_t vmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint16_t vmin(uint16_t a, uint16_t b) { return a < b ? a : b; }

@@ -37,7 +37,9 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_regdec(std::index_sequence<
 template <size_t I>
 hipError_t launch_persist(const RegArgs& a, int ngroups, hipStream_t stream) {
   if constexpr (kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2)
-    return launch_persistent(viterbi_multi_persist<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
+    // lane bits at physical state bits {0, 3}, two periods of decisions in LDS (3 waves per SIMD):
+    // 0.952x the time of the {6, 7} all-VGPR layout (tools/k9_bench.hip, profiles/r03_k9_layouts.txt)
+    return launch_persistent(viterbi_multi_persist<kMultiCodes[I], kPersistBlen, 0, 2, 0, 3>, a, ngroups, stream);
   else
     return hipErrorInvalidValue;
 }
