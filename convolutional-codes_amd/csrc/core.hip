@@ -111,6 +111,7 @@ struct ccv_plan {
   DeviceBuffer counter;              // Fano, stack rows: block work counter
   DeviceBuffer symtab;               // stack rows: expected-symbol table (built on first use)
   DeviceBuffer order;                // Fano, soft: noisiest-first queue order scratch
+  DeviceBuffer park;                 // Fano: parked searches of the two-pass schedule
   bool symtab_ready = false;
   float metric_weight = 0.0f;        // stack, soft: code_param.metric_weight
   int32_t bit_metrics[2] = {0, 0};   // stack, hard: code_param.bit_metrics
@@ -340,6 +341,7 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->counter.release();
   p->symtab.release();
   p->order.release();
+  p->park.release();
   if (p->d_exp) (void)hipFree(p->d_exp);
   if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
@@ -591,8 +593,10 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   if (!d_in || !d_out) return fail("null device buffer");
   if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
   hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
-  if (p->counter.grow(sizeof(unsigned int), stream)) return -1;
-  HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, sizeof(unsigned int), stream));
+  // counters: [0] pass-1 queue, [1] pass-2 queue, [2] parked searches; [4..7] diagnostics
+  if (p->counter.grow(64, stream)) return -1;
+  HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, 64, stream));
+  unsigned int* ctr = static_cast<unsigned int*>(p->counter.ptr);
   ccv::FanoArgs a{};
   a.in = d_in;
   a.n = p->d.n;
@@ -605,12 +609,31 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   a.bm0 = p->bit_metrics[0];
   a.bm1 = p->bit_metrics[1];
   a.nblocks = (int)nblocks;
-  a.next_block = static_cast<unsigned int*>(p->counter.ptr);
+  a.next_block = ctr;
   a.out = d_out;
   a.path_metric = p->d.channel == CCV_HARD ? d_path_metric : nullptr;
   a.info = d_info;
   a.err = d_info ? d_errors : nullptr;
   a.iterations = d_iterations;
+  // two-pass schedule (fano_dev.hpp): park searches after 64 x T moves, resume them in pass 2;
+  // CCV_FANO_CAP=<moves> overrides, 0 = one pass
+  long cap = 64L * a.T;
+  if (const char* env = std::getenv("CCV_FANO_CAP")) cap = std::atol(env);
+  if (cap > 0 && nblocks > 64) {
+    const size_t cap_slots = nblocks / 8 > 65536 ? nblocks / 8 : (nblocks < 65536 ? nblocks : 65536);
+    const size_t mt = p->d.channel == CCV_HARD ? sizeof(int32_t) : sizeof(float);
+    const size_t hdr = cap_slots * ccv::kFanoParkWords * sizeof(uint32_t);
+    const size_t met = (cap_slots * (size_t)(a.T + 1) * mt + 255) & ~(size_t)255;
+    const size_t flg = cap_slots * (size_t)(a.T + 1);
+    if (p->park.grow(hdr + met + flg, stream)) return -1;
+    char* base = static_cast<char*>(p->park.ptr);
+    a.cap = (uint32_t)cap;
+    a.park_capacity = (unsigned int)cap_slots;
+    a.park_count = ctr + 2;
+    a.park_hdr = reinterpret_cast<uint32_t*>(base);
+    a.park_metric = base + hdr;
+    a.park_flags = reinterpret_cast<uint8_t*>(base + hdr + met);
+  }
   if (const char* env = std::getenv("CCV_FANO_COUNT_MOVES")) a.count_moves = env[0] == '1';
   bool tab = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3);
   if (const char* env = std::getenv("CCV_FANO_SYMTAB")) tab = tab && env[0] != '0';
@@ -627,19 +650,26 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
     HIP_TRY(ccv::launch_fano_order(a, p->order.ptr, p->order.bytes, &a.order, stream));
   }
   const bool debug = std::getenv("CCV_FANO_DEBUG") != nullptr;
-  if (debug) {   // diagnostics: synchronous, prints lane utilisation
-    if (p->counter.grow(32, stream)) return -1;
-    a.next_block = static_cast<unsigned int*>(p->counter.ptr);
-    a.stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(p->counter.ptr) + 16);
-    HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, 32, stream));
-  }
+  if (debug)   // diagnostics: synchronous, prints lane utilisation (both passes together)
+    a.stats = reinterpret_cast<unsigned long long*>(ctr + 4);
   HIP_TRY(ccv::launch_fano(a, p->d.channel == CCV_HARD, stream));
+  if (a.cap) {   // pass 2: the parked searches (the count is read on the device)
+    ccv::FanoArgs r = a;
+    r.resume = 1;
+    r.cap = 0;
+    r.next_block = ctr + 1;
+    r.order = nullptr;
+    HIP_TRY(ccv::launch_fano(r, p->d.channel == CCV_HARD, stream));
+  }
   if (debug) {
     unsigned long long st[2] = {0, 0};
+    unsigned int parked = 0;
     HIP_TRY(hipMemcpyAsync(st, a.stats, sizeof st, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(&parked, ctr + 2, sizeof parked, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    std::fprintf(stderr, "fano: %zu blocks, wave passes %llu, busy lane passes %llu, lane utilisation %.3f\n",
-                 nblocks, st[0], st[1], st[0] ? (double)st[1] / (64.0 * (double)st[0]) : 0.0);
+    std::fprintf(stderr, "fano: %zu blocks, %u parked after %u moves, wave passes %llu, busy lane passes %llu, "
+                 "lane utilisation %.3f\n", nblocks, parked, a.cap, st[0], st[1],
+                 st[0] ? (double)st[1] / (64.0 * (double)st[0]) : 0.0);
   }
   return 0;
 }

@@ -7,6 +7,15 @@
 // neighbours finish after ~T steps), so lanes are persistent: a lane that finishes its block takes
 // the next one from a global counter and the wave keeps all 64 lanes busy until the queue drains.
 //
+// Two passes. Lanes pull blocks one at a time, and at 4 dB ~3 % of the searches run into the
+// 10000 x T timeout (540,000 moves at K = 15) while the rest finish in a few hundred: a lane commits
+// to whatever it draws, so over ~150,000 lanes the unluckiest draws six or seven timeouts in a row
+// and the kernel waits for it with its wave nearly empty. Pass 1 therefore parks a search after `cap`
+// moves -- its node path metrics and flags up to the frontier and its registers go to global memory --
+// and takes the next block; pass 2 resumes the parked searches, one per lane, so the time of the
+// long tail is about ONE timeout, not the worst lane's sum of them. A parked search continues from
+// exactly the state it left, so the result is the one-pass result, bit for bit.
+//
 // Per lane, the node array of the reference (:17-25) shrinks to what the search reads back: the
 // path metric of every node (LDS, [T][64] so same-depth accesses are conflict-free) and a flags byte
 // (selected_path, decoded_input). States are re-derived on the way (forward: (s >> 1) | (in << K-2);
@@ -49,7 +58,18 @@ struct FanoArgs {
                              // [1] sum over lanes of passes in which the lane had a search to advance
   const uint16_t* symtab;    // TAB: [2^(K-1)] expected symbols (stack_symtab_init), K <= kSymtabMaxK
   const uint32_t* order;     // optional [nb]: the queue hands out block order[q] (noisiest first)
+  // Two-pass schedule (see fano_decode): pass 1 parks a search after `cap` moves (0 = never) in
+  // slot atomicAdd(park_count); pass 2 (resume = 1, next_block reset) resumes the parked searches.
+  uint32_t cap;
+  int resume;
+  unsigned int park_capacity;   // slots; a search that finds them full keeps running in pass 1
+  unsigned int* park_count;
+  uint32_t* park_hdr;        // [nb][kFanoParkWords]: block, cur, frontier, state, metrics, flags
+  void* park_metric;         // [nb][T + 1] path metrics of the nodes 0..frontier
+  uint8_t* park_flags;       // [nb][T + 1] sel | dec << 1 of the nodes 0..frontier
 };
+
+constexpr int kFanoParkWords = 12;
 
 // Queue order for soft input (launch_fano_order): a search's length is set by the noise in its
 // block, and a few blocks run into the 10000 x T timeout; handed out last, such a block holds its
@@ -185,10 +205,19 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   };
 
   // per-lane search state
-  // the next block from the queue (through the noisiest-first order when there is one)
-  unsigned int b = 0;
+  // the next block from the queue (through the noisiest-first order when there is one), or in the
+  // resume pass the next parked search
+  unsigned int b = 0, slot = 0;
+  unsigned int parked = 0;   // final: pass 1 has completed
+  if (a.resume) parked = *a.park_count < a.park_capacity ? *a.park_count : a.park_capacity;
   auto take = [&]() -> bool {
     const unsigned int q = atomicAdd(a.next_block, 1u);
+    if (a.resume) {
+      if (q >= parked) return false;
+      slot = q;
+      b = a.park_hdr[(size_t)q * kFanoParkWords];
+      return true;
+    }
     if (q >= (unsigned int)a.nblocks) return false;
     b = a.order ? a.order[q] : q;
     return true;
@@ -199,10 +228,43 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   MT mcur = 0, thr = 0, tm0 = 0, tm1 = 0;
   uint32_t sel = 0, dec = 0, timeout = 0;
   bool inback = false, moved = false;
-  uint32_t moves = 0;
+  uint32_t moves = 0, spass = 0;
   FanoRow<HARD, NP> row0{};   // received row of node cur
-  // start a search (:108-124 reset, then the root's branch metrics)
-  auto start = [&]() {
+  auto as_bits = [](MT v) -> uint32_t {
+    if constexpr (HARD) return (uint32_t)v;
+    else return __float_as_uint(v);
+  };
+  auto from_bits = [](uint32_t v) -> MT {
+    if constexpr (HARD) return (MT)(int32_t)v;
+    else return __uint_as_float(v);
+  };
+  // the search at the queue head parks its whole state (the node path metrics and flags up to the
+  // frontier -- the nodes it can read back -- and the registers) for the resume pass
+  auto park = [&]() -> bool {
+    const unsigned int k = atomicAdd(a.park_count, 1u);
+    if (k >= a.park_capacity) return false;
+    uint32_t* h = a.park_hdr + (size_t)k * kFanoParkWords;
+    MT* pm = static_cast<MT*>(a.park_metric) + (size_t)k * (T + 1);
+    uint8_t* pf = a.park_flags + (size_t)k * (T + 1);
+    for (int d = 0; d <= frontier; ++d) {
+      pm[d] = metric[d * kFanoThreads + lane];
+      pf[d] = flags[d * kFanoThreads + lane];
+    }
+    h[0] = b;
+    h[1] = (uint32_t)cur;
+    h[2] = (uint32_t)frontier;
+    h[3] = (uint32_t)(uint64_t)st;
+    h[4] = (uint32_t)((uint64_t)st >> 32);
+    h[5] = as_bits(mcur);
+    h[6] = as_bits(thr);
+    h[7] = as_bits(tm0);
+    h[8] = as_bits(tm1);
+    h[9] = sel | (dec << 1) | ((inback ? 1u : 0u) << 2) | ((moved ? 1u : 0u) << 3);
+    h[10] = timeout;
+    h[11] = moves;
+    return true;
+  };
+  auto load_rows = [&]() {
     rx = in + (size_t)b * T * NS;
     if constexpr (RM == kRowsLds) {
       if constexpr (HARD) {
@@ -213,6 +275,41 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
         for (int d = 0; d < T; ++d) dst[d * kFanoThreads + lane] = src[d];
       }
     }
+  };
+  // resume a parked search exactly where pass 1 left it
+  auto restore = [&]() {
+    load_rows();
+    const uint32_t* h = a.park_hdr + (size_t)slot * kFanoParkWords;
+    cur = (int)h[1];
+    frontier = (int)h[2];
+    const MT* pm = static_cast<const MT*>(a.park_metric) + (size_t)slot * (T + 1);
+    const uint8_t* pf = a.park_flags + (size_t)slot * (T + 1);
+    for (int d = 0; d <= frontier; ++d) {
+      metric[d * kFanoThreads + lane] = pm[d];
+      flags[d * kFanoThreads + lane] = pf[d];
+    }
+    st = (ST)((uint64_t)h[3] | ((uint64_t)h[4] << 32));
+    mcur = from_bits(h[5]);
+    thr = from_bits(h[6]);
+    tm0 = from_bits(h[7]);
+    tm1 = from_bits(h[8]);
+    sel = h[9] & 1u;
+    dec = (h[9] >> 1) & 1u;
+    inback = (h[9] & 4u) != 0;
+    moved = (h[9] & 8u) != 0;
+    timeout = h[10];
+    moves = h[11];
+    spass = 0;
+    if constexpr (ROWS) row0 = row_at(cur);
+  };
+  // start a search (:108-124 reset, then the root's branch metrics)
+  auto start = [&]() {
+    if (a.resume) {
+      restore();
+      return;
+    }
+    load_rows();
+    spass = 0;
     if constexpr (ROWS) row0 = row_at(0);
     metric[lane] = (MT)0;
     cur = 0;
@@ -263,6 +360,14 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   // to the spare node row T.
   for (;;) {
     ++lane_passes;
+    if (__builtin_expect(a.cap != 0 && spass == a.cap, 0)) {   // a long search: resumed in pass 2
+      if (park()) {
+        if (!take()) break;
+        start();
+        continue;
+      }
+    }
+    ++spass;
     // everything a backward move can read, fetched before the move is decided
     const int cm = cur > 0 ? cur - 1 : 0;
     const MT mprev = metric[cm * kFanoThreads + lane];

@@ -127,6 +127,65 @@ def test_fano_queue_order_and_symbol_table_change_nothing(torch_cuda, monkeypatc
     assert np.array_equal(i1, i0)
 
 
+_TWO_PASS = {}
+
+
+def _two_pass_case(channel):
+    """K=15 frames with long searches and timeouts, and the oracle's decode (computed once)."""
+    if channel not in _TWO_PASS:
+        c, nb = K15, 900
+        if channel == SOFT:
+            info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 21)
+            ref, ref_pm = O.fano_soft(_ocode(c), c.fano_metric_weight, rx), None
+        else:
+            info, rx = ch.bsc_blocks(c, nb, 90000, 21)
+            ref, ref_pm = O.fano_hard(_ocode(c), c.fano_bit_metrics, rx)
+        _TWO_PASS[channel] = (info, rx, ref, ref_pm)
+    return _TWO_PASS[channel]
+
+
+@pytest.mark.parametrize("channel", [SOFT, HARD], ids=["soft", "hard"])
+@pytest.mark.parametrize("cap", ["0", "7", "300", "default"])
+def test_fano_two_pass_park_and_resume_is_exact(torch_cuda, monkeypatch, channel, cap):
+    """The two-pass schedule (fano_dev.hpp): searches parked after CCV_FANO_CAP moves and resumed in
+    pass 2 -- after 7 moves nearly every search parks mid-flight (forward runs, look-backs, threshold
+    relaxations), after 300 only the long ones -- give the one-pass (cap 0) outputs, path metrics,
+    error count and per-block search lengths, and the oracle's outputs (K=15, timeouts included)."""
+    torch = torch_cuda
+    if cap == "default":
+        monkeypatch.delenv("CCV_FANO_CAP", raising=False)
+    else:
+        monkeypatch.setenv("CCV_FANO_CAP", cap)
+    c = K15
+    nb = 900
+    info, rx, ref, ref_pm = _two_pass_case(channel)
+    plan = FanoPlan(c, channel)
+    d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+    d_pm = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    d_it = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    plan.decode_fano_device(torch.from_numpy(rx).cuda(), nb, d_out,
+                            d_path_metric=d_pm if channel == HARD else None,
+                            d_info=torch.from_numpy(info).cuda(), d_errors=d_err, d_iterations=d_it)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    assert np.array_equal(out, ref)
+    if channel == HARD:
+        assert np.array_equal(d_pm.cpu().numpy(), ref_pm)
+    assert int(d_err.item()) == ch.count_bit_errors(c, info, out)
+    it = d_it.cpu().numpy()
+    assert (it <= 10000 * c.steps).all()
+    if channel == SOFT:
+        assert (it == 10000 * c.steps).any()
+    # the search lengths equal the one-pass run's
+    monkeypatch.setenv("CCV_FANO_CAP", "0")
+    d_it0 = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    plan.decode_fano_device(torch.from_numpy(rx).cuda(), nb, d_out,
+                            d_path_metric=d_pm if channel == HARD else None, d_iterations=d_it0)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_it0.cpu().numpy(), it)
+
+
 def test_fano_plan_limits():
     with pytest.raises(Exception, match="uint8_t"):
         FanoPlan(K15.with_(blen=250), SOFT)           # T = 264 > 255
