@@ -59,7 +59,8 @@ def core():
     """libccv_core.so: the HIP decoder (include/ccv.h)."""
     if "core" in _cache:
         return _cache["core"]
-    L = _load("libccv_core.so")
+    # CCV_CORE_LIB: an alternative build of the core library in lib/ (kernel A/B builds, tools/)
+    L = _load(os.environ.get("CCV_CORE_LIB", "libccv_core.so"))
     L.ccv_plan_create.argtypes = [_P(_vp), _i, _i, _i, _i, _P(_u64), _i, _u]
     L.ccv_plan_create.restype = _i
     L.ccv_plan_destroy.argtypes = [_vp]

@@ -615,9 +615,12 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   a.info = d_info;
   a.err = d_info ? d_errors : nullptr;
   a.iterations = d_iterations;
-  // two-pass schedule (fano_dev.hpp): park searches after 64 x T moves, resume them in pass 2;
-  // CCV_FANO_CAP=<moves> overrides, 0 = one pass
-  long cap = 64L * a.T;
+  // two-pass schedule (fano_dev.hpp): park searches after 4000 x T moves (0.4 of the timeout), resume
+  // them in pass 2; CCV_FANO_CAP=<moves> overrides, 0 = one pass. Measured caps (tools/fano_caps.py,
+  // profiles/r03_fano_caps.txt; K=15, 104 frames): 4 dB 47.3 (one pass) -> 49.4 Mbit/s at 216,000
+  // moves, but 41.5 at 20,000-108,000 (half the searches park and the parking costs more than the
+  // tail it saves); 6 dB 153 -> 165 at 108,000; BSC 222 -> 239 at 54,000.
+  long cap = 4000L * a.T;
   if (const char* env = std::getenv("CCV_FANO_CAP")) cap = std::atol(env);
   if (cap > 0 && nblocks > 64) {
     const size_t cap_slots = nblocks / 8 > 65536 ? nblocks / 8 : (nblocks < 65536 ? nblocks : 65536);

@@ -7,14 +7,13 @@
 // neighbours finish after ~T steps), so lanes are persistent: a lane that finishes its block takes
 // the next one from a global counter and the wave keeps all 64 lanes busy until the queue drains.
 //
-// Two passes. Lanes pull blocks one at a time, and at 4 dB ~3 % of the searches run into the
-// 10000 x T timeout (540,000 moves at K = 15) while the rest finish in a few hundred: a lane commits
-// to whatever it draws, so over ~150,000 lanes the unluckiest draws six or seven timeouts in a row
-// and the kernel waits for it with its wave nearly empty. Pass 1 therefore parks a search after `cap`
-// moves -- its node path metrics and flags up to the frontier and its registers go to global memory --
-// and takes the next block; pass 2 resumes the parked searches, one per lane, so the time of the
-// long tail is about ONE timeout, not the worst lane's sum of them. A parked search continues from
-// exactly the state it left, so the result is the one-pass result, bit for bit.
+// Two passes. Lanes pull blocks one at a time, and search lengths are heavy-tailed (K = 15 at 4 dB:
+// median 15,000 outer ticks, mean 59,000, 2.7 % run into the 10000 x T = 540,000 timeout): a lane
+// commits to whatever it draws, so the kernel ends with a few lanes finishing long searches in
+// nearly empty waves. Pass 1 therefore parks a search after `cap` moves -- its node path metrics and
+// flags up to the frontier and its registers go to global memory -- and takes the next block; pass 2
+// resumes the parked searches, one per lane, so the long tail runs side by side. A parked search
+// continues from exactly the state it left, so the result is the one-pass result, bit for bit.
 //
 // Per lane, the node array of the reference (:17-25) shrinks to what the search reads back: the
 // path metric of every node (LDS, [T][64] so same-depth accesses are conflict-free) and a flags byte
@@ -304,10 +303,12 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   };
   // start a search (:108-124 reset, then the root's branch metrics)
   auto start = [&]() {
+#ifndef CCV_FANO_NO_PARK
     if (a.resume) {
       restore();
       return;
     }
+#endif
     load_rows();
     spass = 0;
     if constexpr (ROWS) row0 = row_at(0);
@@ -360,6 +361,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   // to the spare node row T.
   for (;;) {
     ++lane_passes;
+#ifndef CCV_FANO_NO_PARK
     if (__builtin_expect(a.cap != 0 && spass == a.cap, 0)) {   // a long search: resumed in pass 2
       if (park()) {
         if (!take()) break;
@@ -367,6 +369,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
         continue;
       }
     }
+#endif
     ++spass;
     // everything a backward move can read, fetched before the move is decided
     const int cm = cur > 0 ? cur - 1 : 0;

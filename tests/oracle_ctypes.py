@@ -167,6 +167,34 @@ def fano_hard(c, fano_bit_metrics, syms):
     return out, pm
 
 
+_fast = None
+
+
+def fast_viterbi(c, data, hard=False, threads=1):
+    """oracle/ccfast.c: the optimised (table-driven, AVX2, pthreads) CPU Viterbi of bench.py's second
+    CPU baseline. Returns (seconds, out[, path metrics])."""
+    global _fast
+    if _fast is None:
+        path = os.path.join(ORACLE_DIR, "build", "libccfast.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.run(["make", "-C", ORACLE_DIR, "oracle"], check=True, capture_output=True)
+        L = ctypes.CDLL(path)
+        L.ccfast_viterbi.argtypes = [ctypes.POINTER(CcoCode), ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.ccfast_viterbi.restype = ctypes.c_double
+        _fast = L
+    data = np.ascontiguousarray(data, dtype=np.uint8 if hard else np.float32)
+    nb = data.shape[0]
+    _, _, OB = dims(c)
+    out = np.zeros((nb, OB), np.uint8)
+    pm = np.zeros(nb, np.int32)
+    t = _fast.ccfast_viterbi(ctypes.byref(c), 1 if hard else 0, _ptr(data), nb, _ptr(out), _ptr(pm), threads)
+    if t < 0:
+        raise ValueError("ccfast_viterbi: unsupported code")
+    return (t, out, pm) if hard else (t, out)
+
+
 def count_errors(c, info, out):
     info = np.ascontiguousarray(info, np.uint8)
     out = np.ascontiguousarray(out, np.uint8)

@@ -142,3 +142,24 @@ def test_oracle_statistical_ber_code0_4dB():
     p = 0.05668375
     # bit errors of a Viterbi decoder come in bursts: allow a generous 5-sigma binomial band
     assert abs(errs / bits - p) < 5 * np.sqrt(p * (1 - p) / bits) * 3
+
+
+@pytest.mark.parametrize("name", ["k7", "k7:true", "code0", "code3", "code5", "k9"])
+@pytest.mark.parametrize("hard", [False, True], ids=["soft", "hard"])
+def test_fast_cpu_decoder_matches_oracle(name, hard):
+    """oracle/ccfast.c (bench.py's optimised CPU baseline) decodes bit for bit like the oracle:
+    ragged group sizes, both generator modes, rate 1/3, K=9; BSC path metrics included."""
+    from ccviterbi import channel as ch, named_code
+    c = named_code(name)
+    oc = O.code(c.n, c.K, c.blen, c.polys, c.gen_mode)
+    nb = 517
+    if hard:
+        _, syms = ch.bsc_blocks(c, nb, 90000, 5)
+        _, out, pm = O.fast_viterbi(oc, syms, hard=True, threads=3)
+        ref, ref_pm = O.viterbi_hard(oc, syms)
+        assert np.array_equal(pm, ref_pm)
+    else:
+        _, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(1.0), 5)
+        _, out = O.fast_viterbi(oc, rx, threads=3)
+        ref = O.viterbi_soft(oc, rx)
+    assert np.array_equal(out, ref)
