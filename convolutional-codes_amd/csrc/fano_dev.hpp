@@ -15,6 +15,13 @@
 // resumes the parked searches, one per lane, so the long tail runs side by side. A parked search
 // continues from exactly the state it left, so the result is the one-pass result, bit for bit.
 //
+// Loop shape matters more than anything in the pass: the block switch (finish, take, start) must stay
+// a branch INSIDE the one pass loop. Written as a `continue` after the switch only, the AMDGPU
+// control-flow structurizer turned the round-2 kernel into a per-block inner loop in which a lane
+// whose search had ended waited, exec-masked, for every other lane of its wave to end theirs (2.3x
+// the time at 4 dB). With the park branch at the top of the pass the compiler keeps
+// one loop.
+//
 // Per lane, the node array of the reference (:17-25) shrinks to what the search reads back: the
 // path metric of every node (LDS, [T][64] so same-depth accesses are conflict-free) and a flags byte
 // (selected_path, decoded_input). States are re-derived on the way (forward: (s >> 1) | (in << K-2);
