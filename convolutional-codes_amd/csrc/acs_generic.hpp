@@ -47,11 +47,12 @@ inline size_t generic_lds_bytes(int n, int K, int T, int chunk, bool hard) {
   return bytes;
 }
 
+// One block, decoded by the whole workgroup (the body of viterbi_generic and of the streaming
+// service kernel viterbi_service).
 template <int SPT, bool HARD>
-__global__ __launch_bounds__(kGenericMaxThreads) void viterbi_generic(GenericArgs a) {
+__device__ __forceinline__ void generic_decode_block(const GenericArgs& a, int b, unsigned char* lds) {
   using MT = typename std::conditional<HARD, uint32_t, float>::type;
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int S = 1 << (a.K - 1), NS = 1 << a.n, T = a.T, b = blockIdx.x;
+  const int S = 1 << (a.K - 1), NS = 1 << a.n, T = a.T;
   const int tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63, wave = tid >> 6;
   const int words = (S + 63) >> 6;
 
@@ -166,6 +167,12 @@ __global__ __launch_bounds__(kGenericMaxThreads) void viterbi_generic(GenericArg
     }
     if (a.err != nullptr && errors) atomicAdd(a.err, (unsigned long long)errors);
   }
+}
+
+template <int SPT, bool HARD>
+__global__ __launch_bounds__(kGenericMaxThreads) void viterbi_generic(GenericArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  generic_decode_block<SPT, HARD>(a, blockIdx.x, lds);
 }
 
 }  // namespace ccv

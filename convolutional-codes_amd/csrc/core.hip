@@ -1,6 +1,7 @@
 // core.hip -- libccv_core.so: plans, kernel selection, launches and the ccv_* C ABI (include/ccv.h).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -9,6 +10,7 @@
 #include <vector>
 
 #include "acs_generic.hpp"
+#include "acs_latency.hpp"
 #include "acs_persist.hpp"
 #include "channel_dev.hpp"
 #include "fano_dev.hpp"
@@ -19,6 +21,7 @@
 
 namespace ccv {
 constexpr size_t kHostLatencyMaxBlocks = 64;   // ccv_decode_host batches decoded by the generic kernel
+constexpr size_t kServiceMaxBlocks = 4;        // ... and by the resident streaming service
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s);   // stack.hip
 bool stack_rows_eligible(int n, int K, int T);                           // stack.hip
 bool stack_symtab_eligible(int n, int K, int T);                         // stack.hip
@@ -78,7 +81,7 @@ struct PinnedBuffer {
   void* host = nullptr;
   void* dev = nullptr;
   size_t bytes = 0;
-  int grow(size_t need, hipStream_t sync_stream) {
+  int grow(size_t need, hipStream_t sync_stream, unsigned flags = hipHostMallocDefault) {
     if (need <= bytes) return 0;
     if (host) {
       HIP_TRY(hipStreamSynchronize(sync_stream));
@@ -86,7 +89,8 @@ struct PinnedBuffer {
       host = dev = nullptr;
       bytes = 0;
     }
-    HIP_TRY(hipHostMalloc(&host, need, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&host, need, flags));
+    memset(host, 0, need);
     HIP_TRY(hipHostGetDevicePointer(&dev, host, 0));
     bytes = need;
     return 0;
@@ -124,6 +128,10 @@ struct ccv_plan {
   DeviceBuffer dec;                  // register-kernel decision scratch
   DeviceBuffer host_in, host_out, host_pm;   // staging for ccv_decode_host
   PinnedBuffer lat_in, lat_out, lat_pm;        // zero-copy staging of small ccv_decode_host calls
+  PinnedBuffer svc_mb, svc_in, svc_out, svc_pm; // streaming service: fine-grained mailbox and staging
+  hipStream_t svc_stream = nullptr;            // the service kernel's own stream
+  bool svc_running = false;
+  uint32_t svc_seq = 0;
   bool generic_ok = false;                     // the generic kernel can run this code (d_exp built)
   DeviceBuffer sim_info, sim_out;             // ccv_simulate_device scratch (caller passed none)
   hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
@@ -217,6 +225,39 @@ hipError_t launch_generic(const ccv::GenericArgs& a, const ccv_plan& p, size_t n
     case 2: return launch_generic_t<2, HARD>(a, p, nblocks, s);
     case 4: return launch_generic_t<4, HARD>(a, p, nblocks, s);
     default: return launch_generic_t<8, HARD>(a, p, nblocks, s);
+  }
+}
+
+bool latency_kernel_ok(const ccv_plan& p) { return p.d.K <= ccv::kLatencyMaxK; }
+
+size_t latency_lds(const ccv_plan& p) {
+  return ccv::latency_lds_bytes(p.d.n, p.d.steps, p.d.channel == CCV_HARD);
+}
+
+template <int SPT, bool HARD, bool LAT>
+hipError_t launch_service_t(const ccv::GenericArgs& a, const ccv_plan& p, ccv::ServiceMailbox* mb,
+                            uint32_t served, hipStream_t s) {
+  const void* fn = reinterpret_cast<const void*>(&ccv::viterbi_service<SPT, HARD, LAT>);
+  const size_t lds = LAT ? latency_lds(p) : p.generic_lds;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  // idle 20 ms of the 100 MHz real-time counter, at most 2,000,000 polls (~2-4 s)
+  hipLaunchKernelGGL((ccv::viterbi_service<SPT, HARD, LAT>), dim3(1), dim3(LAT ? 64 : p.generic_threads), lds, s,
+                     a, mb, served, (uint64_t)2000000, (uint32_t)2000000);
+  return hipGetLastError();
+}
+
+template <bool HARD>
+hipError_t launch_service(const ccv::GenericArgs& a, const ccv_plan& p, ccv::ServiceMailbox* mb,
+                          uint32_t served, hipStream_t s) {
+  if (latency_kernel_ok(p)) return launch_service_t<1, HARD, true>(a, p, mb, served, s);
+  switch (p.generic_spt) {
+    case 1: return launch_service_t<1, HARD, false>(a, p, mb, served, s);
+    case 2: return launch_service_t<2, HARD, false>(a, p, mb, served, s);
+    case 4: return launch_service_t<4, HARD, false>(a, p, mb, served, s);
+    default: return launch_service_t<8, HARD, false>(a, p, mb, served, s);
   }
 }
 
@@ -328,6 +369,16 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
 
 void ccv_plan_destroy(ccv_plan* p) {
   if (!p) return;
+  if (p->svc_stream) {   // end the streaming service kernel (it polls `stop`), then wait for it
+    if (p->svc_mb.host)
+      __atomic_store_n(&static_cast<ccv::ServiceMailbox*>(p->svc_mb.host)->stop, 1u, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(p->svc_stream);
+    (void)hipStreamDestroy(p->svc_stream);
+  }
+  p->svc_mb.release();
+  p->svc_in.release();
+  p->svc_out.release();
+  p->svc_pm.release();
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   p->dec.release();
   p->host_in.release();
@@ -810,6 +861,77 @@ int ccv_stack_decode_host(ccv_plan* p, const void* in, size_t nblocks, const voi
   return 0;
 }
 
+// The streaming path through the resident service kernel (acs_generic.hpp viterbi_service): post the
+// block(s) in the fine-grained mailbox, relaunch the kernel if it has ended (idle timeout), spin on
+// `done`. One block costs two PCIe round trips and the decode, no launch.
+static int decode_host_service(ccv_plan* p, const void* in, size_t nblocks, uint8_t* out,
+                               int32_t* path_metric) {
+  const bool hard = p->d.channel == CCV_HARD;
+  const size_t in_bytes = nblocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes;
+  const size_t out_bytes = nblocks * (size_t)p->d.out_bytes;
+  if (!p->svc_stream) HIP_TRY(hipStreamCreateWithFlags(&p->svc_stream, hipStreamNonBlocking));
+  if (p->svc_mb.grow(sizeof(ccv::ServiceMailbox), p->svc_stream, hipHostMallocCoherent)) return -1;
+  ccv::ServiceMailbox* mb = static_cast<ccv::ServiceMailbox*>(p->svc_mb.host);
+  if (p->svc_in.bytes < in_bytes || p->svc_out.bytes < out_bytes || p->svc_pm.bytes < nblocks * 4) {
+    // the resident kernel holds the old buffers: end it before they are replaced
+    if (p->svc_running) {
+      __atomic_store_n(&mb->stop, 1u, __ATOMIC_RELEASE);
+      HIP_TRY(hipStreamSynchronize(p->svc_stream));
+      __atomic_store_n(&mb->stop, 0u, __ATOMIC_RELEASE);
+      p->svc_running = false;
+    }
+    const size_t cap_blocks = ccv::kServiceMaxBlocks;
+    if (p->svc_in.grow(cap_blocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes, p->svc_stream,
+                       hipHostMallocCoherent) ||
+        p->svc_out.grow(cap_blocks * (size_t)p->d.out_bytes, p->svc_stream, hipHostMallocCoherent) ||
+        p->svc_pm.grow(cap_blocks * sizeof(int32_t), p->svc_stream, hipHostMallocCoherent))
+      return -1;
+  }
+  memcpy(p->svc_in.host, in, in_bytes);
+  ccv::GenericArgs a{};
+  a.in = p->svc_in.dev;
+  a.exp = p->d_exp;
+  a.n = p->d.n;
+  a.K = p->d.K;
+  a.T = p->d.steps;
+  a.blen = p->d.blen;
+  a.nblocks = (int)nblocks;
+  a.chunk = p->generic_chunk;
+  a.out = static_cast<uint8_t*>(p->svc_out.dev);
+  a.path_metric = hard ? static_cast<int32_t*>(p->svc_pm.dev) : nullptr;
+  auto launch = [&](uint32_t served) -> int {
+    __atomic_store_n(&mb->exited, 0u, __ATOMIC_RELEASE);
+    HIP_TRY(hard ? launch_service<true>(a, *p, mb, served, p->svc_stream)
+                 : launch_service<false>(a, *p, mb, served, p->svc_stream));
+    p->svc_running = true;
+    return 0;
+  };
+  const uint32_t seq = ++p->svc_seq;
+  __atomic_store_n(&mb->nblocks, (uint32_t)nblocks, __ATOMIC_RELAXED);
+  if (!p->svc_running || __atomic_load_n(&mb->exited, __ATOMIC_ACQUIRE)) {
+    if (p->svc_running) HIP_TRY(hipStreamSynchronize(p->svc_stream));   // the ended kernel is gone
+    if (launch(seq - 1)) return -1;
+  }
+  __atomic_store_n(&mb->req, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spins = 0; __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) != seq; ++spins) {
+    if (__atomic_load_n(&mb->exited, __ATOMIC_ACQUIRE) && __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) != seq) {
+      // it reached its idle timeout just before the request arrived: wait for it to end, relaunch
+      HIP_TRY(hipStreamSynchronize(p->svc_stream));
+      if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) break;
+      if (launch(seq - 1)) return -1;
+    }
+    if ((spins & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      p->svc_running = false;
+      return fail("streaming service did not answer within 10 s");
+    }
+    __builtin_ia32_pause();
+  }
+  memcpy(out, p->svc_out.host, out_bytes);
+  if (hard && path_metric) memcpy(path_metric, p->svc_pm.host, nblocks * sizeof(int32_t));
+  return 0;
+}
+
 // Small host batches (the streaming decoder_input path completes one block per call): the input is
 // copied into page-locked memory the kernel reads directly, the generic kernel (one workgroup per
 // block, a few microseconds) writes the output and path metrics straight into page-locked memory, and
@@ -835,8 +957,15 @@ static int decode_host_latency(ccv_plan* p, const void* in, size_t nblocks, uint
   a.chunk = p->generic_chunk;
   a.out = static_cast<uint8_t*>(p->lat_out.dev);
   a.path_metric = hard ? static_cast<int32_t*>(p->lat_pm.dev) : nullptr;
-  HIP_TRY(hard ? launch_generic<true>(a, *p, nblocks, p->stream)
-               : launch_generic<false>(a, *p, nblocks, p->stream));
+  if (latency_kernel_ok(*p)) {   // one wave per block (acs_latency.hpp)
+    const size_t lds = latency_lds(*p);
+    if (hard) hipLaunchKernelGGL((ccv::viterbi_latency<true>), dim3((unsigned)nblocks), dim3(64), lds, p->stream, a);
+    else hipLaunchKernelGGL((ccv::viterbi_latency<false>), dim3((unsigned)nblocks), dim3(64), lds, p->stream, a);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hard ? launch_generic<true>(a, *p, nblocks, p->stream)
+                 : launch_generic<false>(a, *p, nblocks, p->stream));
+  }
   HIP_TRY(hipStreamSynchronize(p->stream));
   memcpy(out, p->lat_out.host, out_bytes);
   if (hard && path_metric) memcpy(path_metric, p->lat_pm.host, nblocks * sizeof(int32_t));
@@ -849,8 +978,12 @@ int ccv_decode_host(ccv_plan* p, const void* in, size_t nblocks, uint8_t* out, i
   if (nblocks == 0) return 0;
   if (!in || !out) return fail("null host buffer");
   if (nblocks <= ccv::kHostLatencyMaxBlocks && p->generic_ok && !p->stack && !p->fano) {
+    // CCV_HOST_LATENCY: 2 (default) the resident service kernel for up to kServiceMaxBlocks blocks,
+    // 1 a launch per call on zero-copy staging, 0 the device-staged batch path (A/B)
     const char* env = std::getenv("CCV_HOST_LATENCY");
-    if (!env || env[0] != '0') return decode_host_latency(p, in, nblocks, out, path_metric);
+    const int mode = env && env[0] ? env[0] - '0' : 2;
+    if (mode >= 2 && nblocks <= ccv::kServiceMaxBlocks) return decode_host_service(p, in, nblocks, out, path_metric);
+    if (mode >= 1) return decode_host_latency(p, in, nblocks, out, path_metric);
   }
   const size_t in_bytes = nblocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes;
   const size_t out_bytes = nblocks * (size_t)p->d.out_bytes;

@@ -572,6 +572,39 @@ def test_reference_driver_with_mi355x_decoder(case, tmp_path):
     assert int(meta["errors"]) == case["errors"]
 
 
+@pytest.mark.parametrize("channel", [SOFT, HARD], ids=["soft", "hard"])
+def test_streaming_service_kernel(channel, monkeypatch):
+    """The resident streaming service (acs_generic.hpp viterbi_service, ccv_decode_host with <= 4
+    blocks): many single-block calls, 1-4-block calls, pauses past the kernel's 20 ms idle exit (so it
+    is relaunched) and the launch-per-call and staged paths (CCV_HOST_LATENCY=1 / 0) all give the
+    oracle's output and path metrics."""
+    import time
+    c = K7 if channel == SOFT else CODEBOOK[0]
+    nb = 120
+    if channel == SOFT:
+        _, data = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 77)
+    else:
+        _, data = ch.bsc_blocks(c, nb, 80000, 77)
+    ref, ref_pm = _oracle(c, channel, data)
+    for mode in ("2", "1", "0"):
+        monkeypatch.setenv("CCV_HOST_LATENCY", mode)
+        plan = Plan(c, channel)
+        k = 0
+        sizes = [1] * 40 + [2, 3, 4, 1, 4, 3, 2] * 4
+        for i, n in enumerate(sizes):
+            if k + n > nb:
+                break
+            if i in (10, 41):
+                time.sleep(0.05)   # past the service's idle exit: the next call relaunches it
+            res = plan.decode_host(data[k:k + n])
+            out = res if channel == SOFT else res[0]
+            assert np.array_equal(out, ref[k:k + n]), (mode, i)
+            if channel == HARD:
+                assert np.array_equal(res[1], ref_pm[k:k + n]), (mode, i)
+            k += n
+        plan.close()   # stops a service kernel that is still polling
+
+
 def test_streaming_shim_latency_config1(tmp_path):
     """Config 1 (BSC K=3 code 0, 10 k bits = 250 blocks) through the reference drivers' call pattern
     (one decoder_input() per trellis step, oracle/ref_harness.c linked to libccv_bsc.so): output equal

@@ -2,11 +2,12 @@
 """Per-block latency of the streaming decoder_input() path (the reference drivers' call pattern,
 AWGN-channel/main.c:114, binary-symmetric-channel/main.c:70: one trellis step per call, the block
 decoded and the callback fired inside the call that completes it).
+MI355X rows: CCV_HOST_LATENCY=2 (default: the resident service kernel polling a host mailbox), 1 (a
+generic-kernel launch per block on zero-copy staging), 0 (device staging + the register kernel).
 
 Runs oracle/ref_harness_*_ccv (the reference drivers' producer chain linked to the MI355X shims) and
 oracle/ref_harness_* (the same chain linked to the reference decoder) and reads `decoder_seconds`
-(wall time inside decoder_input) from their .meta files. MI355X rows run twice: the zero-copy
-generic-kernel path (default) and CCV_HOST_LATENCY=0 (device staging + register kernel).
+(wall time inside decoder_input) from their .meta files.
 usage: shim_latency.py [NBLOCKS] > table"""
 import os
 import subprocess
@@ -38,7 +39,8 @@ def main():
         t_ref, nb, blen, ref_out = run(os.path.join(REF, f"ref_harness_{chan}"), nblocks, param, spec)
         print(f"{name:34s} {'reference decoder (CPU, 1 thread)':34s} {t_ref / nb * 1e6:9.2f} "
               f"{nb * blen / t_ref / 1e6:8.2f} -")
-        for mode, label in (("1", "MI355X shim, zero-copy generic"), ("0", "MI355X shim, staged register")):
+        for mode, label in (("2", "MI355X shim, resident service"), ("1", "MI355X shim, launch per block"),
+                            ("0", "MI355X shim, staged register")):
             env = dict(os.environ, CCV_HOST_LATENCY=mode)
             t, nb, blen, out = run(os.path.join(REF, f"ref_harness_{chan}_ccv"), nblocks, param, spec, env)
             print(f"{name:34s} {label:34s} {t / nb * 1e6:9.2f} {nb * blen / t / 1e6:8.2f} {out == ref_out}")
