@@ -228,23 +228,36 @@ hipError_t launch_generic(const ccv::GenericArgs& a, const ccv_plan& p, size_t n
   }
 }
 
-bool latency_kernel_ok(const ccv_plan& p) { return p.d.K <= ccv::kLatencyMaxK; }
+bool latency_kernel_ok(const ccv_plan& p) { return p.d.K >= 2 && p.d.K <= ccv::kLatencyMaxK; }
+
+template <bool HARD>
+void launch_latency(const ccv::GenericArgs& a, const ccv_plan& p, int nblocks, size_t lds) {
+  const dim3 g((unsigned)nblocks), b(64);
+  switch (p.d.K - 1) {
+    case 1: hipLaunchKernelGGL((ccv::viterbi_latency<HARD, 1>), g, b, lds, p.stream, a); break;
+    case 2: hipLaunchKernelGGL((ccv::viterbi_latency<HARD, 2>), g, b, lds, p.stream, a); break;
+    case 3: hipLaunchKernelGGL((ccv::viterbi_latency<HARD, 3>), g, b, lds, p.stream, a); break;
+    case 4: hipLaunchKernelGGL((ccv::viterbi_latency<HARD, 4>), g, b, lds, p.stream, a); break;
+    case 5: hipLaunchKernelGGL((ccv::viterbi_latency<HARD, 5>), g, b, lds, p.stream, a); break;
+    default: hipLaunchKernelGGL((ccv::viterbi_latency<HARD, 6>), g, b, lds, p.stream, a); break;
+  }
+}
 
 size_t latency_lds(const ccv_plan& p) {
   return ccv::latency_lds_bytes(p.d.n, p.d.steps, p.d.channel == CCV_HARD);
 }
 
-template <int SPT, bool HARD, bool LAT>
+template <int SPT, bool HARD, int LATN>
 hipError_t launch_service_t(const ccv::GenericArgs& a, const ccv_plan& p, ccv::ServiceMailbox* mb,
                             uint32_t served, hipStream_t s) {
-  const void* fn = reinterpret_cast<const void*>(&ccv::viterbi_service<SPT, HARD, LAT>);
-  const size_t lds = LAT ? latency_lds(p) : p.generic_lds;
+  const void* fn = reinterpret_cast<const void*>(&ccv::viterbi_service<SPT, HARD, LATN>);
+  const size_t lds = LATN ? latency_lds(p) : p.generic_lds;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   // idle 20 ms of the 100 MHz real-time counter, at most 2,000,000 polls (~2-4 s)
-  hipLaunchKernelGGL((ccv::viterbi_service<SPT, HARD, LAT>), dim3(1), dim3(LAT ? 64 : p.generic_threads), lds, s,
+  hipLaunchKernelGGL((ccv::viterbi_service<SPT, HARD, LATN>), dim3(1), dim3(LATN ? 64 : p.generic_threads), lds, s,
                      a, mb, served, (uint64_t)2000000, (uint32_t)2000000);
   return hipGetLastError();
 }
@@ -252,12 +265,21 @@ hipError_t launch_service_t(const ccv::GenericArgs& a, const ccv_plan& p, ccv::S
 template <bool HARD>
 hipError_t launch_service(const ccv::GenericArgs& a, const ccv_plan& p, ccv::ServiceMailbox* mb,
                           uint32_t served, hipStream_t s) {
-  if (latency_kernel_ok(p)) return launch_service_t<1, HARD, true>(a, p, mb, served, s);
+  if (latency_kernel_ok(p)) {
+    switch (p.d.K - 1) {
+      case 1: return launch_service_t<1, HARD, 1>(a, p, mb, served, s);
+      case 2: return launch_service_t<1, HARD, 2>(a, p, mb, served, s);
+      case 3: return launch_service_t<1, HARD, 3>(a, p, mb, served, s);
+      case 4: return launch_service_t<1, HARD, 4>(a, p, mb, served, s);
+      case 5: return launch_service_t<1, HARD, 5>(a, p, mb, served, s);
+      default: return launch_service_t<1, HARD, 6>(a, p, mb, served, s);
+    }
+  }
   switch (p.generic_spt) {
-    case 1: return launch_service_t<1, HARD, false>(a, p, mb, served, s);
-    case 2: return launch_service_t<2, HARD, false>(a, p, mb, served, s);
-    case 4: return launch_service_t<4, HARD, false>(a, p, mb, served, s);
-    default: return launch_service_t<8, HARD, false>(a, p, mb, served, s);
+    case 1: return launch_service_t<1, HARD, 0>(a, p, mb, served, s);
+    case 2: return launch_service_t<2, HARD, 0>(a, p, mb, served, s);
+    case 4: return launch_service_t<4, HARD, 0>(a, p, mb, served, s);
+    default: return launch_service_t<8, HARD, 0>(a, p, mb, served, s);
   }
 }
 
@@ -907,12 +929,11 @@ static int decode_host_service(ccv_plan* p, const void* in, size_t nblocks, uint
     return 0;
   };
   const uint32_t seq = ++p->svc_seq;
-  __atomic_store_n(&mb->nblocks, (uint32_t)nblocks, __ATOMIC_RELAXED);
   if (!p->svc_running || __atomic_load_n(&mb->exited, __ATOMIC_ACQUIRE)) {
     if (p->svc_running) HIP_TRY(hipStreamSynchronize(p->svc_stream));   // the ended kernel is gone
     if (launch(seq - 1)) return -1;
   }
-  __atomic_store_n(&mb->req, seq, __ATOMIC_RELEASE);
+  __atomic_store_n(&mb->req, ((uint64_t)nblocks << 32) | seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spins = 0; __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) != seq; ++spins) {
     if (__atomic_load_n(&mb->exited, __ATOMIC_ACQUIRE) && __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) != seq) {
@@ -959,8 +980,8 @@ static int decode_host_latency(ccv_plan* p, const void* in, size_t nblocks, uint
   a.path_metric = hard ? static_cast<int32_t*>(p->lat_pm.dev) : nullptr;
   if (latency_kernel_ok(*p)) {   // one wave per block (acs_latency.hpp)
     const size_t lds = latency_lds(*p);
-    if (hard) hipLaunchKernelGGL((ccv::viterbi_latency<true>), dim3((unsigned)nblocks), dim3(64), lds, p->stream, a);
-    else hipLaunchKernelGGL((ccv::viterbi_latency<false>), dim3((unsigned)nblocks), dim3(64), lds, p->stream, a);
+    if (hard) launch_latency<true>(a, *p, (int)nblocks, lds);
+    else launch_latency<false>(a, *p, (int)nblocks, lds);
     HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hard ? launch_generic<true>(a, *p, nblocks, p->stream)

@@ -605,12 +605,45 @@ def test_streaming_service_kernel(channel, monkeypatch):
         plan.close()   # stops a service kernel that is still polling
 
 
+# The one-wave latency kernel (acs_latency.hpp) has two shapes: register exchange for T <= 64 and
+# decision masks + a traceback beyond; every K it serves (2..7), both sides of T = 64, tied inputs.
+K2 = Code(2, 2, 40, (0xC000000000000000, 0x8000000000000000), GEN_REF_X86)
+LATENCY_CODES = [("k2", K2), ("code0", CODEBOOK[0]), ("code1", CODEBOOK[1]), ("code2", CODEBOOK[2]),
+                 ("code3", CODEBOOK[3]), ("code5_r13", CODEBOOK[5]), ("k7", K7),
+                 ("k7_true", K7.with_(gen_mode=GEN_TRUE_PARITY))]
+LATENCY_BLENS = [1, 5, 40, 57, 58, 59, 100, 255]   # K=7: T = 7, 11, 46, 63, 64, 65, 106, 261
+
+
+@pytest.mark.parametrize("blen", LATENCY_BLENS)
+@pytest.mark.parametrize("name,base", LATENCY_CODES, ids=[x[0] for x in LATENCY_CODES])
+def test_latency_kernel_shapes(name, base, blen, monkeypatch):
+    c = base.with_(blen=blen)
+    monkeypatch.setenv("CCV_HOST_LATENCY", "1")            # one launch per call, one wave per block
+    nb = 48
+    _, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 31 + blen)
+    tied = np.random.default_rng(blen).integers(-2, 3, size=rx.shape).astype(np.float32)
+    _, syms = ch.bsc_blocks(c, nb, 90000, 31 + blen)
+    plan_s, plan_h = Plan(c, SOFT), Plan(c, HARD)
+    for data in (rx, tied):
+        assert np.array_equal(plan_s.decode_host(data), O.viterbi_soft(_ocode(c), data))
+    out, pm = plan_h.decode_host(syms)
+    ref, ref_pm = O.viterbi_hard(_ocode(c), syms)
+    assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+    monkeypatch.setenv("CCV_HOST_LATENCY", "2")            # the resident service, <= 4 blocks a call
+    plan_s2 = Plan(c, SOFT)
+    for k in range(0, 12, 3):
+        assert np.array_equal(plan_s2.decode_host(tied[k:k + 3]), O.viterbi_soft(_ocode(c), tied[k:k + 3]))
+    plan_s2.close()
+    plan_s.close()
+    plan_h.close()
+
+
 def test_streaming_shim_latency_config1(tmp_path):
     """Config 1 (BSC K=3 code 0, 10 k bits = 250 blocks) through the reference drivers' call pattern
     (one decoder_input() per trellis step, oracle/ref_harness.c linked to libccv_bsc.so): output equal
     to the reference decoder's on the same stream, and the time spent inside decoder_input() reported
-    (.meta decoder_seconds) -- each completed block costs one generic-kernel launch on zero-copy
-    staging and one synchronise (INTEGRATION.md states the measured microseconds per block)."""
+    (.meta decoder_seconds) -- each completed block is decoded by the resident service kernel
+    (INTEGRATION.md states the measured microseconds per block)."""
     import os
     import subprocess
     from conftest import REPO
