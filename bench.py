@@ -409,8 +409,13 @@ def main(argv=None):
         # the binding resource, from the measured fractions: HBM traffic vs VALU issue
         if traffic_frac is not None and valu_frac is not None:
             bound = "valu" if valu_frac > traffic_frac else "hbm"
+            bound_basis = ("the larger of traffic_frac (PMC HBM bytes / kernel time / 8 TB/s) and "
+                           "valu_frac (SQ_INSTS_VALU / (512 per cycle x GRBM_GUI_ACTIVE / 8)); "
+                           "frac / achieved / peak stay the SURVEY 8(d) HBM figure")
         else:
-            bound = "hbm" if not sequential and traffic_frac is not None else "valu"
+            bound = None   # not derived: no committed PMC pass for this workload
+            bound_basis = (f"unmeasured: no PMC pass committed for workload key {workload_key!r} "
+                           "(profiles/pmc_workloads.json; tools/pmc_workload.sh adds one)")
         cpu = cpu_opt = None
         if world == 1 and not args.no_cpu_baseline:
             gpu_out = d_out.cpu().numpy()
@@ -478,9 +483,7 @@ def main(argv=None):
                 "clock_ghz": (round(pmc["grbm_gui_active"] / 8 / (pmc["kernel_ns"] * 1e-9) / 1e9, 3)
                               if pmc.get("grbm_gui_active") and pmc.get("kernel_ns") else None),
                 "pmc_source": pmc.get("source"),
-                "bound_basis": "the larger of traffic_frac (PMC HBM bytes / kernel time / 8 TB/s) and "
-                               "valu_frac (SQ_INSTS_VALU / (512 per cycle x GRBM_GUI_ACTIVE / 8)); "
-                               "frac / achieved / peak stay the SURVEY 8(d) HBM figure",
+                "bound_basis": bound_basis,
             },
             "cpu_baseline": cpu,
             "cpu_baseline_optimized": cpu_opt,
