@@ -342,7 +342,9 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+    step_ms = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
+    kernel_ms = sum(step_ms) / args.steps
+    kernel_ms_median = step_ms[len(step_ms) // 2]
 
     errs = d_err.clone()   # the timed steps' error count (the informational runs below add more)
 
@@ -361,6 +363,24 @@ def main(argv=None):
             h_out.copy_(d_out, non_blocking=True)
         torch.cuda.synchronize()
         pcie_s = (time.perf_counter() - t1) / reps
+
+    # informational: the measured HBM copy ceiling: a device-to-device copy of the
+    # input batch, read + write bytes over the copy's event time, best of 5
+    copy_gbs = None
+    if rank == 0:
+        dst = torch.empty_like(d_rx)
+        dst.copy_(d_rx)
+        best = None
+        for _ in range(5):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(stream)
+            dst.copy_(d_rx)
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            ms = ev[0].elapsed_time(ev[1])
+            best = ms if best is None else min(best, ms)
+        copy_gbs = 2 * d_rx.numel() * d_rx.element_size() / (best * 1e-3) / 1e9
+        del dst
 
     # informational: the same frames generated AND decoded on the GPU (ccv_simulate_device, the
     # on-device channel of SURVEY.md 8(f) #1) -- no host producer, no input in HBM
@@ -463,6 +483,7 @@ def main(argv=None):
                     "errors": errors, "bits": bits_per_step * args.steps,
                     "ber": errors / (bits_per_step * args.steps)},
             "kernel_ms": round(kernel_ms, 4),
+            "kernel_ms_median": round(kernel_ms_median, 4),
             "per_rank_kernel_ms": per_rank_kernel_ms,
             "clock_warmup_s": args.clock_warmup,
             "pcie_inclusive_mbit_s": round(nb * code.blen / pcie_s / 1e6, 1) if pcie_s else None,
@@ -483,6 +504,9 @@ def main(argv=None):
                 "clock_ghz": (round(pmc["grbm_gui_active"] / 8 / (pmc["kernel_ns"] * 1e-9) / 1e9, 3)
                               if pmc.get("grbm_gui_active") and pmc.get("kernel_ns") else None),
                 "pmc_source": pmc.get("source"),
+                "copy_ceiling_gbs": round(copy_gbs, 1) if copy_gbs else None,
+                "traffic_of_copy_ceiling": (round(traffic / (kernel_ms * 1e-3) / 1e9 / copy_gbs, 4)
+                                            if traffic and copy_gbs else None),
                 "bound_basis": bound_basis,
             },
             "cpu_baseline": cpu,
