@@ -194,6 +194,20 @@ def load_pmc(workload_key):
         return {}
 
 
+def pmc_for_variant(pmc, variant):
+    """The PMC record only if it was taken on the kernel this plan runs (a record of another kernel
+    for the same workload key -- e.g. the K = 9 four-lane kernel before the one-lane-per-block one --
+    is stale and reported as unmeasured)."""
+    kernel = pmc.get("kernel", "")
+    if not kernel:
+        return pmc
+    if variant == "persistent-wide":
+        return pmc if "viterbi_wide_persist" in kernel else {}
+    if variant == "persistent":
+        return pmc if "_persist<" in kernel and "wide" not in kernel else {}
+    return pmc
+
+
 def valu_fraction(pmc):
     """Issued VALU wave-instructions over the chip's issue capacity in the same cycles: a wave64 VALU
     instruction issues over 2 cycles on a 32-lane CDNA4 SIMD (MI355X_MICROARCH.md), so 1,024 SIMDs
@@ -416,13 +430,15 @@ def main(argv=None):
         # comparable"); hbm_bytes_per_bit counts only what must cross HBM for this kernel (decisions
         # excluded where they stay in VGPRs / LDS), and the PMC traffic what did cross it.
         bpb = algorithmic_bytes_per_bit(code, soft=not hard, decisions=not sequential)
+        # ("slot": the K = 9 one-lane kernel's per-wave scratch, L2 / Infinity-Cache resident, counted
+        # as HBM bytes here; the PMC traffic says what actually crossed)
         on_chip = sequential or getattr(plan, "decisions", "hbm") in ("registers", "lds")
         hbm_bpb = algorithmic_bytes_per_bit(code, soft=not hard, decisions=not on_chip)
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         hbm_achieved = hbm_bpb * nb * code.blen / (kernel_ms * 1e-3) / 1e9
         workload_key = workload_key_of(args)
-        pmc = load_pmc(workload_key)
+        pmc = pmc_for_variant(load_pmc(workload_key), getattr(plan, "variant", ""))
         traffic = pmc.get("hbm_bytes_per_launch")
         traffic_frac = traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None
         valu_frac = valu_fraction(pmc)

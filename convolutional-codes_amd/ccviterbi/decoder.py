@@ -75,8 +75,9 @@ class Plan:
 
     @property
     def decisions(self):
-        """Where survivor decisions live during a decode: "none", "hbm", "registers" or "lds"."""
-        return {0: "none", 1: "hbm", 2: "registers", 3: "lds"}[self._lib.ccv_plan_decision_storage(self._h)]
+        """Where survivor decisions live during a decode: "none", "hbm", "registers", "lds" or "slot"
+        (a per-wave scratch slot, include/ccv.h CCV_DECISIONS_SLOT)."""
+        return {0: "none", 1: "hbm", 2: "registers", 3: "lds", 4: "slot"}[self._lib.ccv_plan_decision_storage(self._h)]
 
     @property
     def variant(self):

@@ -165,12 +165,22 @@ ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
   return ccv::soft_regdec_launchers()[p.reg_index];
 }
 
-// The persistent K <= 7 kernel (acs_persist.hpp), or nullptr: codebook block length, block-major
-// input, decisions not exported.
+// The one-lane-per-block persistent K = 9 kernel (acs_wide.hpp; the x86-idiom code, soft), or
+// nullptr: codebook block length, block-major input, decisions not exported.
+ccv::RegLaunchFn wide_kernel(const ccv_plan& p, bool export_decisions) {
+  if (p.no_persistent || p.global_decisions || export_decisions || p.step_major ||
+      p.d.blen != ccv::kPersistBlen || p.multi_index < 0 || p.d.channel != CCV_SOFT)
+    return nullptr;
+  return ccv::multi_wide_launchers()[p.multi_index];
+}
+
+// The persistent kernel (acs_persist.hpp K <= 7, acs_wide.hpp / acs_multi.hpp K = 9), or nullptr:
+// codebook block length, block-major input, decisions not exported.
 ccv::RegLaunchFn persist_kernel(const ccv_plan& p, bool export_decisions) {
   if (p.no_persistent || p.global_decisions || export_decisions || p.step_major ||
       p.d.blen != ccv::kPersistBlen)
     return nullptr;
+  if (const ccv::RegLaunchFn wide = wide_kernel(p, export_decisions)) return wide;
   if (p.multi_index >= 0)
     return p.d.channel == CCV_SOFT ? ccv::multi_persist_launchers()[p.multi_index] : nullptr;
   if (p.reg_index < 0) return nullptr;
@@ -436,6 +446,7 @@ int ccv_plan_decision_storage(const ccv_plan* p) {
   if (!p) return fail("null plan");
   if (p->stack || p->fano) return CCV_DECISIONS_NONE;
   if (!register_path(*p)) return CCV_DECISIONS_LDS;   // acs_generic.hpp: a block's decisions in LDS
+  if (wide_kernel(*p, false)) return CCV_DECISIONS_SLOT;
   return persist_kernel(*p, false) || regdec_kernel(*p, false) ? CCV_DECISIONS_REGISTERS
                                                                : CCV_DECISIONS_HBM;
 }
@@ -445,16 +456,17 @@ const char* ccv_plan_kernel_variant(const ccv_plan* p) {
   if (p->stack) return "stack";
   if (p->fano) return "fano";
   if (!register_path(*p)) return "generic";
+  if (wide_kernel(*p, false)) return "persistent-wide";
   if (persist_kernel(*p, false)) return "persistent";
   if (p->multi_index >= 0) return regdec_kernel(*p, false) ? "multilane-regdec" : "multilane";
   return regdec_kernel(*p, false) ? "register-regdec" : "register";
 }
 
-int ccv_plan_persistent_waves(const ccv_plan* p, int fresh) {
-  if (!p) return fail("null plan");
-  const ccv::RegLaunchFn persist = persist_kernel(*p, false);
-  if (!persist) return 0;
-  ccv::g_persist_query = ccv::PersistQuery{true, fresh != 0, 0};
+namespace {
+// Grid of a persistent launcher (resident waves): the launcher runs in query mode and launches
+// nothing. -1 on error.
+int persistent_grid(ccv::RegLaunchFn persist, bool fresh) {
+  ccv::g_persist_query = ccv::PersistQuery{true, fresh, 0};
   ccv::RegArgs a{};
   const hipError_t e = persist(a, 1, nullptr);
   const int waves = ccv::g_persist_query.waves;
@@ -463,8 +475,24 @@ int ccv_plan_persistent_waves(const ccv_plan* p, int fresh) {
   return waves;
 }
 
+// The wide kernel's decision scratch: one slot per resident wave (acs_wide.hpp).
+int grow_wide_scratch(ccv_plan& p, ccv::RegLaunchFn wide, hipStream_t stream) {
+  const int waves = persistent_grid(wide, false);
+  if (waves <= 0) return waves < 0 ? -1 : fail("no resident waves for the K = 9 kernel");
+  return p.dec.grow((size_t)waves * ccv::multi_wide_slot_bytes(), stream);
+}
+}  // namespace
+
+int ccv_plan_persistent_waves(const ccv_plan* p, int fresh) {
+  if (!p) return fail("null plan");
+  const ccv::RegLaunchFn persist = persist_kernel(*p, false);
+  if (!persist) return 0;
+  return persistent_grid(persist, fresh != 0);
+}
+
 int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {
   if (!p) return fail("null plan");
+  if (const ccv::RegLaunchFn wide = wide_kernel(*p, false)) return grow_wide_scratch(*p, wide, p->stream);
   if (persist_kernel(*p, false)) {
     // hard: a partial last group of < 64 blocks runs on viterbi_hard_reg with HBM decisions
     if (p->d.channel != CCV_HARD) return 0;
@@ -506,6 +534,13 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     a.path_metric = hard ? d_path_metric : nullptr;
     a.info = d_info;
     a.err = d_info ? d_errors : nullptr;
+    if (const ccv::RegLaunchFn wide = wide_kernel(*p, d_decisions != nullptr)) {
+      // one lane per block, groups of 64 blocks, decisions in a per-wave scratch slot (acs_wide.hpp)
+      if (grow_wide_scratch(*p, wide, stream)) return -1;
+      a.dec = p->dec.ptr;
+      HIP_TRY(wide(a, (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads), stream));
+      return 0;
+    }
     if (const ccv::RegLaunchFn persist = persist_kernel(*p, d_decisions != nullptr)) {
       // decisions in VGPRs, grid = resident waves walking groups of 64 / lanes blocks
       // (acs_persist.hpp, acs_multi.hpp)

@@ -65,6 +65,13 @@ int multi_regdec_max_steps(int K);
 // groups of 64 / 2^(K-7) blocks), nullptr where a code has none (K = 9, r = 1/2 only); valid for
 // blen == kPersistBlen, block-major input, no decision export (reg_multi.hip)
 const RegLaunchFn* multi_persist_launchers();
+// [kNumMultiCodes] one-lane-per-block persistent soft kernel (acs_wide.hpp viterbi_wide_persist;
+// int argument = groups of 64 blocks), nullptr where a code has none (the K = 9 x86-idiom code:
+// 156 distinct metrics fit one lane's VGPRs; the true-parity trellis has 256). RegArgs::dec = one
+// scratch slot of multi_wide_slot_bytes() per resident wave of the grid. Valid for blen ==
+// kPersistBlen, block-major input, no decision export (reg_multi.hip)
+const RegLaunchFn* multi_wide_launchers();
+size_t multi_wide_slot_bytes();
 
 struct ChanArgs;
 using ChanLaunchFn = hipError_t (*)(const ChanArgs&, int grid, hipStream_t stream);

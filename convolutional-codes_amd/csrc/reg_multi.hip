@@ -4,6 +4,7 @@
 #include <utility>
 
 #include "acs_multi.hpp"
+#include "acs_wide.hpp"
 #include "reg_codes.hpp"
 
 namespace ccv {
@@ -49,8 +50,26 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence
   return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2) ? &launch_persist<I> : nullptr)...};
 }
 
+template <size_t I>
+hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
+  // one lane per block, decisions through a per-wave scratch slot: 0.65x the time of the four-lane
+  // kernel below at 32 frames, bit-identical (tools/k9_bench.hip, profiles/r03_k9_wide.txt)
+  if constexpr (kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2 && kMultiCodes[I].gen == GEN_REF_X86)
+    return launch_persistent(viterbi_wide_persist<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
+  else
+    return hipErrorInvalidValue;
+}
+
+template <size_t... I>
+constexpr std::array<RegLaunchFn, sizeof...(I)> make_wide(std::index_sequence<I...>) {
+  return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2 && kMultiCodes[I].gen == GEN_REF_X86)
+               ? &launch_wide<I>
+               : nullptr)...};
+}
+
 constexpr auto kSoft = make<false>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kSoftPersist = make_persist(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kSoftWide = make_wide(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kHard = make<true>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kSoftRegDec = make_regdec<false>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kHardRegDec = make_regdec<true>(std::make_index_sequence<kNumMultiCodes>{});
@@ -60,6 +79,10 @@ constexpr auto kHardRegDec = make_regdec<true>(std::make_index_sequence<kNumMult
 const RegLaunchFn* multi_launchers(bool hard) { return hard ? kHard.data() : kSoft.data(); }
 
 const RegLaunchFn* multi_persist_launchers() { return kSoftPersist.data(); }
+
+const RegLaunchFn* multi_wide_launchers() { return kSoftWide.data(); }
+
+size_t multi_wide_slot_bytes() { return wide_slot_bytes(kPersistBlen); }
 
 const RegLaunchFn* multi_regdec_launchers(bool hard) {
   return hard ? kHardRegDec.data() : kSoftRegDec.data();

@@ -79,16 +79,19 @@ int ccv_plan_trellis(const ccv_plan* plan, uint8_t* exp);
  * CCV_DECISIONS_NONE (stack / Fano decoders: no trellis), CCV_DECISIONS_HBM (scratch array in device
  * memory, read back by the traceback), CCV_DECISIONS_REGISTERS (VGPR-resident for the whole block:
  * the persistent K <= 7 kernels at blen 40, soft r = 1/2 codes with K <= 7 and blen + K - 1 <= 48,
- * K = 8, 9 with short blocks) or CCV_DECISIONS_LDS (the generic kernel keeps a block's decisions in
- * LDS). */
+ * K = 8, 9 with short blocks), CCV_DECISIONS_LDS (the generic kernel keeps a block's decisions in
+ * LDS) or CCV_DECISIONS_SLOT (the K = 9 one-lane-per-block kernel: a scratch slot per resident wave,
+ * rewritten by every group the wave decodes, so it stays in the L2 / Infinity Cache working set). */
 #define CCV_DECISIONS_NONE 0
 #define CCV_DECISIONS_HBM 1
 #define CCV_DECISIONS_REGISTERS 2
 #define CCV_DECISIONS_LDS 3
+#define CCV_DECISIONS_SLOT 4
 int ccv_plan_decision_storage(const ccv_plan* plan);
 
 /* Name of the kernel a ccv_decode_device call without decision export runs: "persistent",
- * "register-regdec", "register", "multilane-regdec", "multilane", "generic", "stack" or "fano". */
+ * "persistent-wide" (K = 9, one lane per block), "register-regdec", "register", "multilane-regdec",
+ * "multilane", "generic", "stack" or "fano". */
 const char* ccv_plan_kernel_variant(const ccv_plan* plan);
 
 /* Grid (resident waves = occupancy x CUs, whole SIMDs) of the plan's persistent kernel: the value

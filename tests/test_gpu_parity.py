@@ -91,8 +91,11 @@ def test_register_kernel_selected_for_benchmark_codes():
     assert Plan(K7, SOFT, FLAG_GENERIC).decisions == "lds"          # acs_generic.hpp
     # K = 8, 9 (multilane kernel): register-resident up to T = 48 (K9) / 49 (K8), soft and hard
     for c in (K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
-        assert Plan(c, SOFT).decisions == "registers" and Plan(c, HARD).decisions == "registers"
+        # the K = 9 x86-idiom soft code runs one lane per block with a per-wave decision slot
+        soft = "slot" if c is K9 else "registers"
+        assert Plan(c, SOFT).decisions == soft and Plan(c, HARD).decisions == "registers"
         assert Plan(c, SOFT, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
+        assert Plan(c, SOFT, FLAG_NO_PERSISTENT).decisions == "registers"
     assert Plan(K9.with_(blen=41), SOFT).decisions == "hbm"           # T = 49
     assert Plan(K8.with_(blen=42), SOFT).decisions == "registers"     # T = 49
     # a K=9 code without an ahead-of-time kernel falls back to the table-driven kernel
@@ -281,7 +284,7 @@ def test_persistent_grid_per_kernel(torch_cuda):
     plans = [(K7, SOFT), (CODEBOOK[0], HARD), (K9, SOFT)]
     for c, channel in plans:
         p = Plan(c, channel)
-        assert p.variant == "persistent"
+        assert p.variant == ("persistent-wide" if c is K9 else "persistent")
         nb = 3 * 64 + 5
         if channel == SOFT:
             info, data = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 5)
@@ -348,6 +351,29 @@ def test_multilane_shapes(K, nb, blen):
         assert np.array_equal(plan.decode_host(rx), O.viterbi_soft(_ocode(c), rx))
         out, pm = Plan(c, HARD, flags).decode_host(syms)
         assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+
+
+@pytest.mark.parametrize("nb", [1, 63, 64, 65, 3 * 64 + 5, 150000])
+def test_k9_wide_kernel(torch_cuda, nb):
+    """K = 9 x86-idiom soft at blen 40 runs the one-lane-per-block kernel (acs_wide.hpp): ragged
+    batches and more 64-block groups than resident waves (150,000 blocks: each wave decodes several
+    groups through its one decision slot) decode exactly as the four-lane kernel (FLAG_NO_PERSISTENT)
+    and, on a sample, the oracle; the fused error count equals the host count."""
+    torch = torch_cuda
+    plan = Plan(K9, SOFT)
+    assert plan.variant == "persistent-wide" and plan.decisions == "slot"
+    info, rx = ch.awgn_blocks(K9, nb, ch.noise_scaling(3.0), 4242 + nb)
+    d_out = torch.empty((nb, K9.out_bytes), dtype=torch.uint8, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    plan.decode_device(_device(torch, rx), nb, d_out, d_info=_device(torch, info), d_errors=d_err)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    assert int(d_err.item()) == ch.count_bit_errors(K9, info, out)
+    four_lane = Plan(K9, SOFT, FLAG_NO_PERSISTENT)
+    assert four_lane.variant.startswith("multilane")
+    assert np.array_equal(out, four_lane.decode_host(rx))
+    sample = np.unique(np.linspace(0, nb - 1, min(nb, 300)).astype(np.int64))
+    assert np.array_equal(out[sample], O.viterbi_soft(_ocode(K9), rx[sample]))
 
 
 def test_multilane_error_count_and_no_decision_export(torch_cuda):

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "acs_multi.hpp"
+#include "acs_wide.hpp"
 #include "reg_codes.hpp"
 
 using namespace ccv;
@@ -50,6 +51,34 @@ double run(const char* name, RegArgs a, int ngroups, int cus) {
   ms /= 40;
   const double bits = (double)a.nblocks * 40;
   printf("%-34s waves/CU %2d  %.4f ms  %6.2f Gbit/s\n", name, per_cu, ms, bits / (ms * 1e-3) / 1e9);
+  fflush(stdout);
+  return ms;
+}
+
+// the one-lane-per-block kernel (acs_wide.hpp), decisions in a per-wave global scratch slot
+template <int AB = 0>
+double run_wide(const char* name, RegArgs a, int ngroups, int cus) {
+  auto kern = viterbi_wide_persist<kK9, 40, AB>;
+  ngroups = (a.nblocks + 63) / 64;   // 64-block groups (one lane per block)
+  int per_cu = 0;
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
+  if (per_cu >= 4) per_cu -= per_cu % 4;
+  const int grid = per_cu * cus < ngroups ? per_cu * cus : ngroups;
+  static void* scratch = nullptr;
+  if (!scratch) CHECK(hipMalloc(&scratch, (size_t)grid * wide_slot_bytes(40)));
+  a.dec = scratch;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int rep = 0; rep < 100; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, a, ngroups);
+  CHECK(hipEventRecord(e0, 0));
+  for (int rep = 0; rep < 40; ++rep) hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, a, ngroups);
+  CHECK(hipEventRecord(e1, 0));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= 40;
+  printf("%-34s waves/CU %2d  %.4f ms  %6.2f Gbit/s\n", name, per_cu, ms, (double)a.nblocks * 40 / (ms * 1e-3) / 1e9);
   fflush(stdout);
   return ms;
 }
@@ -137,24 +166,34 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(o2.data(), d_out2, o2.size(), hipMemcpyDeviceToHost));
     if (memcmp(o1.data(), o2.data(), o1.size()) != 0) printf("   OUTPUTS DIFFER\n");
   };
-  // round-robin repeats: the clock drifts over a run, so candidates are interleaved and the median
-  // of each one's repeats is compared
-  std::vector<std::vector<double>> t(7);
-  const char* names[7] = {"production {6,7}", "{0,3} LDS x2", "{0,5} LDS x2", "{2,5}", "{2,5} LDS x3",
-                          "{4,7} LDS x2", "{0,3}"};
-  for (int round = 0; round < 5; ++round) {
-    t[0].push_back(run<0>(names[0], a, ngroups, cus));
-    t[1].push_back(run<0, 2, 0, 3>(names[1], c, ngroups, cus)); check();
-    t[2].push_back(run<0, 2, 0, 5>(names[2], c, ngroups, cus)); check();
-    t[3].push_back(run<0, 0, 2, 5>(names[3], c, ngroups, cus)); check();
-    t[4].push_back(run<0, 3, 2, 5>(names[4], c, ngroups, cus)); check();
-    t[5].push_back(run<0, 2, 4, 7>(names[5], c, ngroups, cus)); check();
-    t[6].push_back(run<0, 0, 0, 3>(names[6], c, ngroups, cus)); check();
+  const bool wide_only = argc > 2 && strcmp(argv[2], "wide") == 0;
+  {
+    std::vector<std::vector<double>> t(2);
+    const char* names[2] = {"production {0,3} LDS x2", "one lane per block (wide)"};
+    for (int round = 0; round < (wide_only ? 1 : 5); ++round) {
+      t[0].push_back(run<0, 2, 0, 3>(names[0], a, ngroups, cus));
+      CHECK(hipMemcpy(o1.data(), d_out, o1.size(), hipMemcpyDeviceToHost));
+      t[1].push_back(run_wide(names[1], c, ngroups, cus)); check();
+    }
+    printf("medians (relative to production):\n");
+    auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+    for (int k = 0; k < 2; ++k) printf("  %-26s %.4f ms  %.3f\n", names[k], med(t[k]), med(t[k]) / med(t[0]));
+    {
+      std::vector<std::vector<double>> tw(4);
+      const char* wn[4] = {"wide", "wide, input nt", "wide, traceback loads nt", "wide, both nt"};
+      for (int round = 0; round < 5; ++round) {
+        tw[0].push_back(run_wide<0>(wn[0], c, ngroups, cus)); check();
+        tw[1].push_back(run_wide<4>(wn[1], c, ngroups, cus)); check();
+        tw[2].push_back(run_wide<8>(wn[2], c, ngroups, cus)); check();
+        tw[3].push_back(run_wide<12>(wn[3], c, ngroups, cus)); check();
+      }
+      for (int k = 0; k < 4; ++k) printf("  %-26s %.4f ms  %.3f\n", wn[k], med(tw[k]), med(tw[k]) / med(tw[0]));
+    }
+    run_wide<1>("wide, no decision stores", c, ngroups, cus);
+    run_wide<2>("wide, no traceback loads", c, ngroups, cus);
+    run_wide<3>("wide, neither", c, ngroups, cus);
+    if (wide_only) return 0;
   }
-  printf("medians (relative to production):\n");
-  auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
-  for (int k = 0; k < 7; ++k)
-    printf("  %-20s %.4f ms  %.3f\n", names[k], med(t[k]), med(t[k]) / med(t[0]));
   run<kMultiNoTraceback>("no traceback", a, ngroups, cus);
   run<kMultiNoMem>("no input traffic", a, ngroups, cus);
   run<kMultiNoMem | kMultiNoTraceback>("no input, no traceback", a, ngroups, cus);
