@@ -125,6 +125,8 @@ __device__ __forceinline__ uint32_t argmin_wide(const float (&M)[S]) {
 // 64 lanes is one contiguous KiB).
 constexpr size_t wide_slot_bytes(int main_steps) { return (size_t)main_steps * 2 * kRegThreads * 16; }
 
+// ABLATE (timing studies, tools/k9_bench.hip; production 0): 1 decisions discarded, 2 no traceback
+// loads, 4 input with the default cache policy, 16 drain the decision stores before the traceback.
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void viterbi_wide_persist(RegArgs a, int ngroups) {
@@ -165,8 +167,10 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
       for (int k = 0; k < UPR; ++k) {
         const int r = k * (kRegThreads / UPR) + ln / UPR, j = ln % UPR;
         const uint32_t off = (uint32_t)r * block_bytes + (uint32_t)(j ^ ((r / GRP) % UPR)) * 16;
+        // nt (aux 2): the input is read once; 0.976x the time of the default policy (the decision
+        // slots keep more of the caches, profiles/r03_k9_wide.txt); AB & 4: default policy
         __builtin_amdgcn_global_load_lds(base + off, (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16), 16, 0,
-                                         (ABLATE & 4) ? 2 : 0);
+                                         (ABLATE & 4) ? 0 : 2);
       }
     } else {
 #pragma unroll
@@ -248,37 +252,50 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
     // final state (its bits are the outputs of the last K-1 steps) and takes the decision of main
     // step m (the output of step m) at the bottom; its low K-1 bits are always the current state.
     uint64_t h = argmin_wide<S>(M);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this group's decision stores are in L2
-    constexpr int HALF = BLEN / 2;
-    auto walk = [&]<int m0>() __attribute__((always_inline)) {   // main steps m0 + HALF - 1 .. m0
-      u32x4 dw[HALF][2];
+    // The decision words come back in quarters of the block, two quarters in flight: a quarter is
+    // walked while the next one loads (the loads queue behind this wave's own stores to the same
+    // addresses, which they therefore see; AB & 16: drain the stores first, as the first cut did).
+    if constexpr ((ABLATE & 16) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    constexpr int Q = BLEN / 4;
+    static_assert(BLEN % 4 == 0, "quarters");
+    u32x4 dw[2][Q][2];
+    auto load_quarter = [&]<int qi>() __attribute__((always_inline)) {   // main steps qi*Q .. qi*Q+Q-1
 #pragma unroll
-      for (int i = 0; i < HALF; ++i) {
+      for (int i = 0; i < Q; ++i) {
         if constexpr ((ABLATE & 2) != 0) {   // timing ablation: no decision loads
-          dw[i][0] = u32x4{(uint32_t)i, 1u, 2u, 3u};
-          dw[i][1] = u32x4{4u, 5u, 6u, (uint32_t)i};
-          asm volatile("" : "+v"(dw[i][0]), "+v"(dw[i][1]));
+          dw[qi & 1][i][0] = u32x4{(uint32_t)i, 1u, 2u, 3u};
+          dw[qi & 1][i][1] = u32x4{4u, 5u, 6u, (uint32_t)i};
+          asm volatile("" : "+v"(dw[qi & 1][i][0]), "+v"(dw[qi & 1][i][1]));
         } else {
-          dw[i][0] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, (2 * (m0 + i)) * 1024, (ABLATE & 8) ? 2 : 0);
-          dw[i][1] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, (2 * (m0 + i) + 1) * 1024, (ABLATE & 8) ? 2 : 0);
+          dw[qi & 1][i][0] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, (2 * (qi * Q + i)) * 1024, 0);
+          dw[qi & 1][i][1] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, (2 * (qi * Q + i) + 1) * 1024, 0);
         }
       }
+    };
+    auto walk_quarter = [&]<int qi>() __attribute__((always_inline)) {   // steps qi*Q+Q-1 .. qi*Q
 #pragma unroll
-      for (int i = HALF - 1; i >= 0; --i) {
+      for (int i = Q - 1; i >= 0; --i) {
+        const u32x4 lo = dw[qi & 1][i][0], hi = dw[qi & 1][i][1];
         const uint32_t st = (uint32_t)h;
         const uint32_t m5 = (uint32_t)__builtin_amdgcn_sbfe((int)st, 5, 1);   // 0 / -1 per state bit
         const uint32_t m6 = (uint32_t)__builtin_amdgcn_sbfe((int)st, 6, 1);
         const uint32_t m7 = (uint32_t)__builtin_amdgcn_sbfe((int)st, 7, 1);
-        const uint32_t l0 = select_v(m5, dw[i][0].y, dw[i][0].x), l1 = select_v(m5, dw[i][0].w, dw[i][0].z);
-        const uint32_t l2 = select_v(m5, dw[i][1].y, dw[i][1].x), l3 = select_v(m5, dw[i][1].w, dw[i][1].z);
+        const uint32_t l0 = select_v(m5, lo.y, lo.x), l1 = select_v(m5, lo.w, lo.z);
+        const uint32_t l2 = select_v(m5, hi.y, hi.x), l3 = select_v(m5, hi.w, hi.z);
         const uint32_t k0 = select_v(m6, l1, l0), k1 = select_v(m6, l3, l2);
         const uint32_t word = select_v(m7, k1, k0);
         const uint32_t dbit = __builtin_amdgcn_ubfe(word, st & 31u, 1);
         h = (h << 1) | dbit;
       }
     };
-    walk.template operator()<HALF>();
-    walk.template operator()<0>();
+    load_quarter.template operator()<3>();
+    load_quarter.template operator()<2>();
+    walk_quarter.template operator()<3>();
+    load_quarter.template operator()<1>();
+    walk_quarter.template operator()<2>();
+    load_quarter.template operator()<0>();
+    walk_quarter.template operator()<1>();
+    walk_quarter.template operator()<0>();
     const uint64_t bits = __builtin_bitreverse64(h);   // bit 63 - t = output of step t
     if (b < nb) {
       const uint8_t* info = a.info + (size_t)b * IB;

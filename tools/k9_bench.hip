@@ -180,18 +180,16 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 2; ++k) printf("  %-26s %.4f ms  %.3f\n", names[k], med(t[k]), med(t[k]) / med(t[0]));
     {
       std::vector<std::vector<double>> tw(4);
-      const char* wn[4] = {"wide", "wide, input nt", "wide, traceback loads nt", "wide, both nt"};
+      const char* wn[4] = {"wide", "wide, input default policy", "wide, stores drained first", "wide, no traceback loads"};
       for (int round = 0; round < 5; ++round) {
         tw[0].push_back(run_wide<0>(wn[0], c, ngroups, cus)); check();
         tw[1].push_back(run_wide<4>(wn[1], c, ngroups, cus)); check();
-        tw[2].push_back(run_wide<8>(wn[2], c, ngroups, cus)); check();
-        tw[3].push_back(run_wide<12>(wn[3], c, ngroups, cus)); check();
+        tw[2].push_back(run_wide<16>(wn[2], c, ngroups, cus)); check();
+        tw[3].push_back(run_wide<2>(wn[3], c, ngroups, cus));
       }
       for (int k = 0; k < 4; ++k) printf("  %-26s %.4f ms  %.3f\n", wn[k], med(tw[k]), med(tw[k]) / med(tw[0]));
     }
     run_wide<1>("wide, no decision stores", c, ngroups, cus);
-    run_wide<2>("wide, no traceback loads", c, ngroups, cus);
-    run_wide<3>("wide, neither", c, ngroups, cus);
     if (wide_only) return 0;
   }
   run<kMultiNoTraceback>("no traceback", a, ngroups, cus);

@@ -46,6 +46,9 @@ def avg(xs):
     return sum(xs) / len(xs) if xs else None
 
 
+GUIDE_READ_SCALE, GUIDE_WRITE_SCALE = 2.0, 1.0
+
+
 def main():
     root, out_json = sys.argv[1], sys.argv[2]
     ap = argparse.ArgumentParser()
@@ -74,7 +77,11 @@ def main():
         "kernel": dec_k,
         "launches_profiled": len(durs[dec_k]),
         "kernel_ns": avg(sq_durs.get(dec_k, durs[dec_k])),
-        "hbm_bytes_per_launch": int(d_fetch * read_scale + d_write * write_scale),
+        # the guide's correction (MI355X_MICROARCH.md HBM/rocprofv3: FETCH_SIZE x 2 on gfx950,
+        # WRITE_SIZE exact); the copy calibration is kept as a cross-check only (it drifted to
+        # 2.67 / 1.33 in runs whose copy was 614 MB, where the K = 9 decode's own bytes -- input +
+        # decision slot, read and written -- match the guide's scales exactly)
+        "hbm_bytes_per_launch": int(d_fetch * GUIDE_READ_SCALE + d_write * GUIDE_WRITE_SCALE),
         "raw_fetch_bytes_per_launch": d_fetch, "raw_write_bytes_per_launch": d_write,
         "calibration": {"copy_kernel": copy_k[0], "copy_bytes": copy_bytes, "read_scale": read_scale,
                         "write_scale": write_scale},
