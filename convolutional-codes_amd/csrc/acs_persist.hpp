@@ -207,7 +207,7 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
              kPersistDepth2 = 16, kPersistLineChunks = 32, kPersistNoMemRandom = 64,
-             kPersistNoDma = 128, kPersistNoLdsRead = 256 };
+             kPersistNoDma = 128, kPersistNoLdsRead = 256, kPersistInputNt = 512 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -301,7 +301,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
 #pragma unroll
       for (int k = 0; k < UPR; ++k)
         __builtin_amdgcn_global_load_lds(base + dma_off[k], (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16),
-                                         16, 0, 0);
+                                         16, 0, (ABLATE & kPersistInputNt) ? 2 : 0);
     } else {
 #pragma unroll
       for (int k = 0; k < UPR; ++k) {

@@ -108,7 +108,7 @@ float sustained(RegArgs a, int ngroups, int waves_per_cu, int cus, int n) {
 
 // Paired A/B: production (A) against each variant (B) in ABBA blocks of 40 launches, so a linear
 // clock/thermal drift cancels; the ratio B/A per block quadruple, mean and spread over 4 quadruples.
-int ab(RegArgs a, int ng, int cus) {
+int ab(RegArgs a, int ng, int cus, bool only_first = false) {
   sustained<kK7Ref, 0>(a, ng, 8, cus, 300);   // clock warm-up
   RegArgs a42 = a;
   a42.T = 48;
@@ -118,7 +118,8 @@ int ab(RegArgs a, int ng, int cus) {
   const float scale42 = (float)((double)ng * 40 / ((double)ng42 * 42));   // per blen-40 bit
   auto A = [&]() { return sustained<kK7Ref, 0>(a, ng, 8, cus, 40); };
   struct V { const char* name; float (*f)(RegArgs, int, int, int, int); bool b42; };
-  const V vs[] = {
+  const V vs_all[] = {
+    {"input nt (aux 2)", sustained<kK7Ref, kPersistInputNt>, false},
     {"2-deep DMA", sustained<kK7Ref, kPersistDepth2>, false},
     {"no DMA (stale LDS rows)", sustained<kK7Ref, kPersistNoDma>, false},
     {"DMA, no LDS reads (synth)", sustained<kK7Ref, kPersistNoLdsRead>, false},
@@ -131,7 +132,9 @@ int ab(RegArgs a, int ng, int cus) {
   };
   double asum = 0;
   int an = 0;
-  for (const V& v : vs) {
+  const int nv = only_first ? 1 : (int)(sizeof(vs_all) / sizeof(vs_all[0]));
+  for (int vi = 0; vi < nv; ++vi) {
+    const V& v = vs_all[vi];
     double r[4], rs = 0, lo = 1e9, hi = 0;
     for (int q = 0; q < 4; ++q) {
       auto B = [&]() { return v.b42 ? v.f(a42, ng42, 8, cus, 40) * scale42 : v.f(a, ng, 8, cus, 40); };
@@ -228,6 +231,7 @@ int main(int argc, char** argv) {
   a.out = d_out;
   const int ng = nb / 64;
   if (argc > 1 && std::string(argv[1]) == "ab") return ab(a, ng, cus);
+  if (argc > 1 && std::string(argv[1]) == "abnt") return ab(a, ng, cus, true);   // input nt only
   if (argc > 1 && std::string(argv[1]) == "abh") return ab_hard<1>(cus) | ab_hard<2>(cus);
   if (argc > 1) {   // persist_bench trace [launches]
     const int n = argc > 2 ? atoi(argv[2]) : 300;
