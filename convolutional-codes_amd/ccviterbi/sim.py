@@ -229,8 +229,17 @@ def ber_interval(errors: int, bits: int, z: float = 3.29, burst: float = 1.0):
 
 
 def _parse_points(text: Optional[str], channel: int) -> List[float]:
+    """Comma list, or an inclusive range start:stop[:step] (step 2, the reference's Eb/N0 spacing,
+    AWGN-channel/main.c:193-197, when omitted)."""
     if not text:
         return list(ch.REFERENCE_EBN0_DB if channel == SOFT else ch.REFERENCE_P_PPM)
+    if ":" in text:
+        parts = [float(x) for x in text.split(":")]
+        start, stop, step = parts[0], parts[1], parts[2] if len(parts) > 2 else 2.0
+        if step <= 0 or len(parts) > 3:
+            raise ValueError(f"bad point range {text!r}")
+        n = int(math.floor((stop - start) / step + 1e-9)) + 1
+        return [start + i * step for i in range(max(n, 0))]
     return [float(x) for x in text.split(",") if x.strip()]
 
 
@@ -253,7 +262,8 @@ def main(argv=None, decode=None):
     ap.add_argument("--channel", choices=("awgn", "bsc"), default="awgn")
     ap.add_argument("--decoder", choices=DECODERS, default="viterbi")
     ap.add_argument("--points", default=None,
-                    help="comma-separated Eb/N0 dB (awgn) or p in ppm (bsc); default the reference sweep "
+                    help="comma-separated Eb/N0 dB (awgn) or p in ppm (bsc), or start:stop[:step] (step 2); "
+                         "default the reference sweep "
                          "(AWGN-channel/main.c:150-161, binary-symmetric-channel/main.c:103-109)")
     ap.add_argument("--bits", type=float, default=None,
                     help="info bits per point (default: the reference's schedule, AWGN-channel/main.c:202-211, "

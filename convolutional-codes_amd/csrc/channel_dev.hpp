@@ -429,6 +429,28 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   accumulate_errors(a.r, errors);
 }
 
+// Frames only: one lane per block draws its info bytes and its whole decoder input and writes them
+// to a.info_out / a.ch_out (soft float [nb][T][2^n], 16-byte row stores at n = 2); no decode. The
+// K = 9 sweep decodes these frames with the one-lane-per-block kernel (acs_wide.hpp) instead of
+// running the channel once per lane of a block's four-lane group (viterbi_channel_multi below).
+template <CodeSpec C, bool HARD>
+__global__ __launch_bounds__(kRegThreads) void channel_frames(ChanArgs a) {
+  static_assert(!HARD && C.n == 2, "soft r = 1/2 frames");
+  using Src = ChannelSource<C, HARD>;
+  const int b = blockIdx.x * kRegThreads + threadIdx.x;
+  if (b >= a.r.nblocks) return;
+  Src src;
+  src.init(a, b, true);
+  src.out = nullptr;   // rows are stored here as one 16-byte store each
+  float4* row = reinterpret_cast<float4*>(a.ch_out) + (size_t)b * a.r.T;
+#pragma unroll 1
+  for (int t = 0; t < a.r.T; ++t) {
+    float BM[4];
+    src.next(BM);
+    row[t] = float4{BM[0], BM[1], BM[2], BM[3]};
+  }
+}
+
 // K = 8, 9: multilane kernel (acs_multi.hpp); every lane of a block's group generates the block's
 // input (the same draws), lane q = 0 owns the info and export writes.
 template <CodeSpec C, bool HARD>

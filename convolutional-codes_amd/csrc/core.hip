@@ -134,6 +134,7 @@ struct ccv_plan {
   uint32_t svc_seq = 0;
   bool generic_ok = false;                     // the generic kernel can run this code (d_exp built)
   DeviceBuffer sim_info, sim_out;             // ccv_simulate_device scratch (caller passed none)
+  DeviceBuffer sim_frames;                    // ccv_simulate_device: K = 9 frames ahead of the wide decode
   hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
 };
 
@@ -421,6 +422,7 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->lat_pm.release();
   p->sim_info.release();
   p->sim_out.release();
+  p->sim_frames.release();
   p->counter.release();
   p->symtab.release();
   p->order.release();
@@ -854,7 +856,11 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
     if (p->sim_out.grow(nblocks * (size_t)p->d.out_bytes, stream)) return -1;
     d_out = static_cast<uint8_t*>(p->sim_out.ptr);
   }
-  if (p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
+  // K = 9 x86-idiom soft at blen 40: frames to HBM once per block, then the one-lane-per-block
+  // decode (acs_wide.hpp) with the fused error count -- the multilane channel kernel draws every
+  // block's channel once per lane of its four-lane group
+  const bool frames_path = !hard && wide_kernel(*p, false) != nullptr && std::getenv("CCV_CHANNEL_FUSED") == nullptr;
+  if (!frames_path && p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
   ccv::ChanArgs a{};
   a.r.in = nullptr;
   a.r.T = p->d.steps;
@@ -881,6 +887,17 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   const char* lds_env = std::getenv("CCV_CHANNEL_LDS_DECISIONS");
   const bool lds_dec = lds_env && lds_env[0] ? lds_env[0] == '1' : hard;
   a.global_decisions = (p->global_decisions || !lds_dec) ? 1 : 0;
+  if (frames_path) {
+    void* frames = d_channel;
+    if (!frames) {
+      if (p->sim_frames.grow(nblocks * (size_t)p->d.steps * (size_t)p->d.in_step_bytes, stream)) return -1;
+      frames = p->sim_frames.ptr;
+    }
+    a.ch_out = frames;
+    HIP_TRY(ccv::channel_frames_launchers()[p->multi_index](
+        a, (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads), stream));
+    return ccv_decode_device(p, frames, nblocks, d_out, nullptr, d_info, d_errors, nullptr, stream_v);
+  }
   const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
   const bool multi = p->reg_index < 0;
   HIP_TRY(ccv::channel_launchers(multi, hard)[multi ? p->multi_index : p->reg_index](a, grid, stream));

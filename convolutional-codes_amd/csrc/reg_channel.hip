@@ -41,12 +41,29 @@ constexpr std::array<ChanLaunchFn, sizeof...(I)> make_multi(std::index_sequence<
   return {&launch_multi<I, HARD>...};
 }
 
+template <size_t I>
+hipError_t launch_frames(const ChanArgs& a, int grid, hipStream_t stream) {
+  if constexpr (kMultiCodes[I].n == 2) {
+    hipLaunchKernelGGL((channel_frames<kMultiCodes[I], false>), dim3(grid), dim3(kRegThreads), 0, stream, a);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+template <size_t... I>
+constexpr std::array<ChanLaunchFn, sizeof...(I)> make_frames(std::index_sequence<I...>) {
+  return {&launch_frames<I>...};
+}
+
 constexpr auto kRegSoft = make_reg<false>(std::make_index_sequence<kNumRegCodes>{});
 constexpr auto kRegHard = make_reg<true>(std::make_index_sequence<kNumRegCodes>{});
 constexpr auto kMultiSoft = make_multi<false>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kMultiHard = make_multi<true>(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kFrames = make_frames(std::make_index_sequence<kNumMultiCodes>{});
 
 }  // namespace
+
+const ChanLaunchFn* channel_frames_launchers() { return kFrames.data(); }
 
 const ChanLaunchFn* channel_launchers(bool multi, bool hard) {
   if (multi) return hard ? kMultiHard.data() : kMultiSoft.data();

@@ -77,5 +77,8 @@ struct ChanArgs;
 using ChanLaunchFn = hipError_t (*)(const ChanArgs&, int grid, hipStream_t stream);
 // channel-fused decode kernels: [kNumRegCodes] or [kNumMultiCodes], reg_channel.hip
 const ChanLaunchFn* channel_launchers(bool multi, bool hard);
+// [kNumMultiCodes] frames-only soft channel (channel_dev.hpp channel_frames): info bytes and the
+// decoder input [nb][T][4] written to ChanArgs::info_out / ch_out, grid = one lane per block
+const ChanLaunchFn* channel_frames_launchers();
 
 }  // namespace ccv

@@ -710,7 +710,7 @@ def _simulate(torch, plan, c, seed, first, nb, param, hard_demap=False):
 
 
 CHANNEL_CODES = [("k7", K7), ("k7_true", K7.with_(gen_mode=GEN_TRUE_PARITY)), ("code0", CODEBOOK[0]),
-                 ("code5_r13", CODEBOOK[5]), ("k8", K8), ("k9_true", K9.with_(gen_mode=GEN_TRUE_PARITY)),
+                 ("code5_r13", CODEBOOK[5]), ("k8", K8), ("k9", K9), ("k9_true", K9.with_(gen_mode=GEN_TRUE_PARITY)),
                  ("k9_blen255", K9.with_(blen=255)), ("k7_blen1", K7.with_(blen=1)),
                  # longer blocks (and the LDS-decision kernel's limit: code3 = K=6 at blen 80 fits
                  # its 20 KiB column, K=7 at blen 100 does not)
@@ -775,6 +775,28 @@ def test_device_channel_ber_sweep_matches_host(torch_cuda):
                 assert d.errors == h.errors
             else:
                 assert abs(d.errors - h.errors) <= max(2, h.errors // 1000)
+
+
+def test_device_channel_k9_frames_path_equals_fused(torch_cuda):
+    """K = 9 x86-idiom soft at blen 40: ccv_simulate_device writes the frames (channel_frames) and
+    decodes them with the one-lane-per-block kernel; the fused multilane channel kernel
+    (CCV_CHANNEL_FUSED=1) draws the same frames -- info, decoder input, output and error count are
+    identical, with and without the hard demapper, for ragged batch sizes."""
+    import os
+    for nb, hard_demap in ((1, False), (200, False), (3 * 64 + 5, True)):
+        runs = []
+        for fused in (False, True):
+            if fused:
+                os.environ["CCV_CHANNEL_FUSED"] = "1"
+            try:
+                runs.append(_simulate(torch_cuda, Plan(K9, SOFT), K9, 21, 7000 + nb, nb,
+                                      ch.noise_scaling(2.0), hard_demap=hard_demap))
+            finally:
+                os.environ.pop("CCV_CHANNEL_FUSED", None)
+        a, b = runs
+        for k in (0, 1, 2):
+            assert np.array_equal(a[k], b[k])
+        assert a[4] == b[4]
 
 
 @pytest.mark.parametrize("channel", [SOFT, HARD])

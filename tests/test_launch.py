@@ -145,3 +145,12 @@ def test_ber_interval():
     lo2, hi2 = ber_interval(100, 10 ** 6, burst=4.0)
     assert lo2 < lo and hi2 > hi
     assert ber_interval(0, 10 ** 6)[0] == 0.0
+
+
+def test_point_ranges():
+    """--points takes a comma list or an inclusive start:stop[:step] range (step 2 dB by default,
+    the reference's spacing)."""
+    from ccviterbi.sim import _parse_points
+    assert _parse_points("0:14", 0) == [0.0, 2.0, 4.0, 6.0, 8.0, 10.0, 12.0, 14.0]
+    assert _parse_points("10:14:1", 0) == [10.0, 11.0, 12.0, 13.0, 14.0]
+    assert _parse_points("3,5", 0) == [3.0, 5.0]
