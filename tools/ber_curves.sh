@@ -4,6 +4,7 @@
 # merged into gpurun_out/ber/ber_curves.json (copy to profiles/). Usage: tools/ber_curves.sh [GPUS]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export PYTHONPATH=$PWD/convolutional-codes_amd${PYTHONPATH:+:$PYTHONPATH}
 OUT=gpurun_out/ber
 mkdir -p $OUT
 G=${1:-1}
