@@ -856,10 +856,11 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
     if (p->sim_out.grow(nblocks * (size_t)p->d.out_bytes, stream)) return -1;
     d_out = static_cast<uint8_t*>(p->sim_out.ptr);
   }
-  // K = 9 x86-idiom soft at blen 40: frames to HBM once per block, then the one-lane-per-block
-  // decode (acs_wide.hpp) with the fused error count -- the multilane channel kernel draws every
-  // block's channel once per lane of its four-lane group
-  const bool frames_path = !hard && wide_kernel(*p, false) != nullptr && std::getenv("CCV_CHANNEL_FUSED") == nullptr;
+  // K = 9 soft at blen 40: frames to HBM once per block, then the persistent decode (x86 idiom: one
+  // lane per block, acs_wide.hpp; true parity: acs_multi.hpp) with the fused error count -- the
+  // multilane channel kernel draws every block's channel once per lane of its four-lane group
+  const bool frames_path = !hard && p->multi_index >= 0 && persist_kernel(*p, false) != nullptr &&
+                           std::getenv("CCV_CHANNEL_FUSED") == nullptr;
   if (!frames_path && p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
   ccv::ChanArgs a{};
   a.r.in = nullptr;

@@ -123,9 +123,9 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
  * d_errors and d_channel (export of the decoder input: float [nb][T][2^n] or uint8 [nb][T]) may be
  * NULL; info and output then go to plan-owned scratch. Info bits and BSC symbols are bit-identical
  * to ccv_sim_*; AWGN samples use the device's double log/sin/cos. AWGN scalings must lie in
- * [0, 2^28) (Eb/N0 above -160 dB), else -1. Asynchronous on `stream`. The K = 9 x86-idiom soft code
- * at blen 40 runs as two kernels instead: the frames into d_channel (or plan scratch), then the
- * one-lane-per-block decode (same draws, same results; CCV_CHANNEL_FUSED=1 forces the fused kernel). */
+ * [0, 2^28) (Eb/N0 above -160 dB), else -1. Asynchronous on `stream`. K = 9 soft codes at blen 40
+ * run as two kernels instead: the frames into d_channel (or plan scratch), then the persistent decode
+ * (same draws, same results; CCV_CHANNEL_FUSED=1 forces the fused kernel). */
 #define CCV_CHANNEL_HARD_DEMAP 1u   /* AWGN: common/hard-demapper.c instead of common/demapper.c */
 int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,

@@ -777,19 +777,21 @@ def test_device_channel_ber_sweep_matches_host(torch_cuda):
                 assert abs(d.errors - h.errors) <= max(2, h.errors // 1000)
 
 
-def test_device_channel_k9_frames_path_equals_fused(torch_cuda):
-    """K = 9 x86-idiom soft at blen 40: ccv_simulate_device writes the frames (channel_frames) and
-    decodes them with the one-lane-per-block kernel; the fused multilane channel kernel
-    (CCV_CHANNEL_FUSED=1) draws the same frames -- info, decoder input, output and error count are
-    identical, with and without the hard demapper, for ragged batch sizes."""
+@pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["ref", "true"])
+def test_device_channel_k9_frames_path_equals_fused(torch_cuda, gen):
+    """K = 9 soft at blen 40: ccv_simulate_device writes the frames (channel_frames) and decodes them
+    with the persistent kernel (x86 idiom: one lane per block; true parity: four lanes); the fused
+    multilane channel kernel (CCV_CHANNEL_FUSED=1) draws the same frames -- info, decoder input,
+    output and error count are identical, with and without the hard demapper, for ragged batches."""
     import os
+    c = K9.with_(gen_mode=gen)
     for nb, hard_demap in ((1, False), (200, False), (3 * 64 + 5, True)):
         runs = []
         for fused in (False, True):
             if fused:
                 os.environ["CCV_CHANNEL_FUSED"] = "1"
             try:
-                runs.append(_simulate(torch_cuda, Plan(K9, SOFT), K9, 21, 7000 + nb, nb,
+                runs.append(_simulate(torch_cuda, Plan(c, SOFT), c, 21, 7000 + nb, nb,
                                       ch.noise_scaling(2.0), hard_demap=hard_demap))
             finally:
                 os.environ.pop("CCV_CHANNEL_FUSED", None)
