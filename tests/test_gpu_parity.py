@@ -157,6 +157,24 @@ def test_reference_api_generator_mode_true_parity():
     assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
 
 
+def test_reference_api_k9_batches_and_streaming():
+    """The reference decoder API (libccv_awgn.so) with the K = 9 code: a large batch through
+    decode_blocks (the one-lane-per-block kernel) and single steps through decoder_input (the
+    latency path) give the oracle's bytes; the callbacks fire in block order."""
+    info, rx = ch.awgn_blocks(K9, 3000, ch.noise_scaling(3.0), 606)
+    dec = SoftDecoder()
+    dec.init(K9)
+    out = dec.decode_blocks(rx)
+    sample = np.arange(0, 3000, 10)
+    assert np.array_equal(out[sample], O.viterbi_soft(_ocode(K9), rx[sample]))
+    got = []
+    dec.register_callback(lambda data, n: got.append(data))
+    for b in range(3):
+        for t in range(K9.steps):
+            dec.input(rx[b, t])
+    assert [bytes(x) for x in got] == [out[b].tobytes() for b in range(3)]
+
+
 SEEDED = [
     ("k7_ref_soft", K7, SOFT), ("k7_true_soft", K7.with_(gen_mode=GEN_TRUE_PARITY), SOFT),
     ("k7_ref_hard", K7, HARD), ("k7_true_hard", K7.with_(gen_mode=GEN_TRUE_PARITY), HARD),
