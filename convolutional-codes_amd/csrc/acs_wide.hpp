@@ -38,6 +38,49 @@ constexpr uint32_t collapsed_mask_word(int w) {
   return m;
 }
 
+// Packed decisions (PACK): a collapsed butterfly's upper decision IS its lower one (same candidates
+// by construction), so only the lower words and the non-collapsed upper decisions are stored,
+// densely: K = 9 idiom 128 + 43 bits = 6 words per step instead of 8.
+template <CodeSpec C>
+constexpr int noncollapsed_count() {
+  int n = 0;
+  for (int j = 0; j < (1 << (C.K - 2)); ++j) n += collapsed_butterfly<C>(j) ? 0 : 1;
+  return n;
+}
+template <CodeSpec C>
+constexpr int noncollapsed_rank(int j) {   // non-collapsed butterflies above j (descending order)
+  int r = 0;
+  for (int k = j + 1; k < (1 << (C.K - 2)); ++k) r += collapsed_butterfly<C>(k) ? 0 : 1;
+  return r;
+}
+template <CodeSpec C>
+constexpr int packed_words() {
+  return (1 << (C.K - 2)) / 32 + (noncollapsed_count<C>() + 31) / 32;
+}
+template <CodeSpec C>
+struct PackedPosTable {
+  uint32_t v[(1 << (C.K - 1)) / 4];   // four 8-bit positions (word << 5 | bit) per word
+  constexpr PackedPosTable() : v() {
+    constexpr int H = 1 << (C.K - 2);
+    bool col[H] = {};
+    int rank[H] = {};
+    int nc = 0;
+    for (int j = H - 1; j >= 0; --j) {
+      col[j] = collapsed_butterfly<C>(j);
+      rank[j] = nc;
+      nc += col[j] ? 0 : 1;
+    }
+    for (int ns = 0; ns < 2 * H; ++ns) {
+      uint32_t pos = (uint32_t)(ns < H ? ns : ns - H);
+      if (ns >= H && !col[ns - H]) {
+        const int r = rank[ns - H], w = r / 32, cnt = nc - 32 * w < 32 ? nc - 32 * w : 32;
+        pos = (uint32_t)(((H / 32 + w) << 5) | (cnt - 1 - r % 32));
+      }
+      v[ns / 4] |= pos << (8 * (ns % 4));
+    }
+  }
+};
+
 // m ? a : b with a VGPR mask (v_bitop3 truth table 0xca, acs_reg.hpp select_bits).
 __device__ __forceinline__ uint32_t select_v(uint32_t m, uint32_t a, uint32_t b) {
   uint32_t r;
@@ -48,15 +91,15 @@ __device__ __forceinline__ uint32_t select_v(uint32_t m, uint32_t a, uint32_t b)
 // One trellis step over S = 2^(K-1) > 64 states in one lane: decision word w holds new states
 // 32w .. 32w + 31 (bit k = state 32w + k). Butterfly j (old 2j, 2j+1 -> new j, j + S/2) as acs_step;
 // a collapsed butterfly's upper decision is the lower one's, filled per word by one v_bitop3.
-template <CodeSpec C>
+template <CodeSpec C, bool PACK, int NW>
 __device__ __forceinline__ void acs_step_wide(float (&M)[1 << (C.K - 1)], const float (&BM)[1 << C.n],
-                                              uint32_t (&d)[(1 << (C.K - 1)) / 32]) {
+                                              uint32_t (&d)[NW]) {
   constexpr int S = 1 << (C.K - 1);
   constexpr int H = S / 2;
   constexpr int HW = H / 32;
   float N[S];
 #pragma unroll
-  for (int w = 0; w < 2 * HW; ++w) d[w] = 0;
+  for (int w = 0; w < NW; ++w) d[w] = 0;
   [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
     ([&]() __attribute__((always_inline)) {
       constexpr int j = H - 1 - js;   // descending: state j ends up in bit j % 32 of word j / 32
@@ -67,16 +110,21 @@ __device__ __forceinline__ void acs_step_wide(float (&M)[1 << (C.K - 1)], const 
       N[j] = vmin(a0, a1);
       d[j / 32] = shift_in(d[j / 32], a0, a1);
       N[j + H] = vmin(b0, b1);
-      if constexpr (!collapsed_butterfly<C>(j))
+      if constexpr (PACK && !collapsed_butterfly<C>(j)) {
+        constexpr int w = HW + noncollapsed_rank<C>(j) / 32;
+        d[w] = shift_in(d[w], b0, b1);
+      } else if constexpr (!collapsed_butterfly<C>(j)) {
         d[HW + j / 32] = shift_in_n<collapsed_below_word<C>(j)>(d[HW + j / 32], b0, b1);
+      }
     }(), ...);
   }(std::make_integer_sequence<int, H>{});
-  [&]<int... ws>(std::integer_sequence<int, ws...>) __attribute__((always_inline)) {
-    ([&]() __attribute__((always_inline)) {
-      if constexpr (collapsed_mask_word<C>(ws) != 0)
-        d[HW + ws] = select_bits(collapsed_mask_word<C>(ws), d[ws], d[HW + ws]);
-    }(), ...);
-  }(std::make_integer_sequence<int, HW>{});
+  if constexpr (!PACK)
+    [&]<int... ws>(std::integer_sequence<int, ws...>) __attribute__((always_inline)) {
+      ([&]() __attribute__((always_inline)) {
+        if constexpr (collapsed_mask_word<C>(ws) != 0)
+          d[HW + ws] = select_bits(collapsed_mask_word<C>(ws), d[ws], d[HW + ws]);
+      }(), ...);
+    }(std::make_integer_sequence<int, HW>{});
 #pragma unroll
   for (int s = 0; s < S; ++s) M[s] = N[s];
 }
@@ -123,11 +171,20 @@ __device__ __forceinline__ uint32_t argmin_wide(const float (&M)[S]) {
 
 // Scratch: one slot per wave of the grid, [main step][half][lane][4 words] (a store of four words of
 // 64 lanes is one contiguous KiB).
-constexpr size_t wide_slot_bytes(int main_steps) { return (size_t)main_steps * 2 * kRegThreads * 16; }
+template <CodeSpec C, bool PACK>
+constexpr int wide_words() { return PACK ? packed_words<C>() : (1 << (C.K - 1)) / 32; }
+template <CodeSpec C, bool PACK = false>
+constexpr size_t wide_slot_bytes(int main_steps) {
+  return (size_t)main_steps * kRegThreads * 4 * wide_words<C, PACK>();
+}
 
 // ABLATE (timing studies, tools/k9_bench.hip; production 0): 1 decisions discarded, 2 no traceback
-// loads, 4 input with the default cache policy, 16 drain the decision stores before the traceback.
-template <CodeSpec C, int BLEN, int ABLATE = 0>
+// loads, 4 input with the default cache policy, 16 drain the decision stores before the traceback,
+// 32 packed without the position table (wrong output), 64 packed upper words padded to a dwordx4.
+// PACK (production: true): 6 decision words per step -- the 128 lower ones and the 43 non-collapsed
+// upper ones dense, a state's (word, bit) from a 256-byte LDS table in the traceback -- instead of 8
+// with the collapsed upper bits filled in: 0.90x the time (profiles/r03_k9_wide_packed_ab.txt).
+template <CodeSpec C, int BLEN, int ABLATE = 0, bool PACK = false>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void viterbi_wide_persist(RegArgs a, int ngroups) {
   constexpr int S = 1 << (C.K - 1);
@@ -141,7 +198,11 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   constexpr int T = BLEN + G;
   constexpr int NCH = (T + PF - 1) / PF;
   constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
-  constexpr int W = S / 32;                   // decision words per step
+  constexpr int W = wide_words<C, PACK>();    // decision words per step
+  constexpr int WH = W - 4;                   // upper words
+  static_assert(WH == 2 || WH == 4, "upper words stored as one dwordx2 / dwordx4 per lane");
+  constexpr int WS = (ABLATE & 64) ? 4 : WH;  // upper words as stored (AB & 64: padded to a dwordx4)
+  constexpr int STEPB = kRegThreads * 4 * (4 + WS);   // slot bytes per main step
   static_assert(T % PF == 0 && G == PF, "K = 9 at blen 40: chunk 0 is the growth, 5 main chunks");
   static_assert(T <= 64, "the history fits 64 bits");
   const int lane = threadIdx.x;
@@ -189,10 +250,15 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   // the VGPR offset and the [step][half] row as an SGPR / immediate offset (64-bit addresses per
   // step would cost 80 VGPRs)
   const __amdgpu_buffer_rsrc_t slot = __builtin_amdgcn_make_buffer_rsrc(
-      static_cast<unsigned char*>(a.dec) + (size_t)blockIdx.x * wide_slot_bytes(BLEN), 0,
-      (int)wide_slot_bytes(BLEN), 0x00020000);
-  const int col = lane * 16;
+      static_cast<unsigned char*>(a.dec) + (size_t)blockIdx.x * STEPB * BLEN, 0, STEPB * BLEN, 0x00020000);
+  const int col = lane * 16, colh = lane * 4 * WS;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __shared__ uint32_t ptab[PACK ? S / 4 : 1];
+  if constexpr (PACK) {
+    static constexpr PackedPosTable<C> kPos{};
+    ptab[lane] = kPos.v[lane];
+  }
 
   uint32_t errors = 0;
   int g = blockIdx.x;
@@ -227,14 +293,20 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
           growth_step_wide<C, u>(M, bm);
         } else {
           uint32_t d[W];
-          acs_step_wide<C>(M, bm, d);
+          acs_step_wide<C, PACK, W>(M, bm, d);
           const int m = (c - 1) * PF + u;   // main step
           if constexpr ((ABLATE & 1) != 0) {   // timing ablation: decisions discarded
-            uint32_t x = d[0] ^ d[1] ^ d[2] ^ d[3] ^ d[4] ^ d[5] ^ d[6] ^ d[7];
+            uint32_t x = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) x ^= d[w];
             asm volatile("" ::"v"(x));
           } else {
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[0], d[1], d[2], d[3]}, slot, col, (2 * m) * 1024, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[4], d[5], d[6], d[7]}, slot, col, (2 * m + 1) * 1024, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[0], d[1], d[2], d[3]}, slot, col, m * STEPB, 0);
+            if constexpr (WS == 2)
+              __builtin_amdgcn_raw_buffer_store_b64(u32x2{d[4], d[W > 5 ? 5 : 4]}, slot, colh, m * STEPB + 1024, 0);
+            else
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[4], d[W > 5 ? 5 : 4], d[W > 6 ? 6 : 4], d[W > 7 ? 7 : 4]},
+                                                     slot, colh, m * STEPB + 1024, 0);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -258,33 +330,54 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
     if constexpr ((ABLATE & 16) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     constexpr int Q = BLEN / 4;
     static_assert(BLEN % 4 == 0, "quarters");
-    u32x4 dw[2][Q][2];
+    uint32_t dw[2][Q][W];
     auto load_quarter = [&]<int qi>() __attribute__((always_inline)) {   // main steps qi*Q .. qi*Q+Q-1
 #pragma unroll
       for (int i = 0; i < Q; ++i) {
+        u32x4 lo, hi4 = {};
+        u32x2 hi2 = {};
         if constexpr ((ABLATE & 2) != 0) {   // timing ablation: no decision loads
-          dw[qi & 1][i][0] = u32x4{(uint32_t)i, 1u, 2u, 3u};
-          dw[qi & 1][i][1] = u32x4{4u, 5u, 6u, (uint32_t)i};
-          asm volatile("" : "+v"(dw[qi & 1][i][0]), "+v"(dw[qi & 1][i][1]));
+          lo = u32x4{(uint32_t)i, 1u, 2u, 3u};
+          hi4 = u32x4{4u, 5u, 6u, (uint32_t)i};
+          hi2 = u32x2{4u, (uint32_t)i};
+          asm volatile("" : "+v"(lo), "+v"(hi4), "+v"(hi2));
         } else {
-          dw[qi & 1][i][0] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, (2 * (qi * Q + i)) * 1024, 0);
-          dw[qi & 1][i][1] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, (2 * (qi * Q + i) + 1) * 1024, 0);
+          const int m = qi * Q + i;
+          lo = __builtin_amdgcn_raw_buffer_load_b128(slot, col, m * STEPB, 0);
+          if constexpr (WS == 2) hi2 = __builtin_amdgcn_raw_buffer_load_b64(slot, colh, m * STEPB + 1024, 0);
+          else hi4 = __builtin_amdgcn_raw_buffer_load_b128(slot, colh, m * STEPB + 1024, 0);
+          if constexpr (WS == 4 && WH == 2) hi2 = u32x2{hi4.x, hi4.y};
+        }
+        dw[qi & 1][i][0] = lo.x; dw[qi & 1][i][1] = lo.y; dw[qi & 1][i][2] = lo.z; dw[qi & 1][i][3] = lo.w;
+        if constexpr (WH == 2) {
+          dw[qi & 1][i][4] = hi2.x; dw[qi & 1][i][W > 5 ? 5 : 4] = hi2.y;
+        } else {
+          dw[qi & 1][i][4] = hi4.x; dw[qi & 1][i][W > 5 ? 5 : 4] = hi4.y;
+          dw[qi & 1][i][W > 6 ? 6 : 4] = hi4.z; dw[qi & 1][i][W > 7 ? 7 : 4] = hi4.w;
         }
       }
     };
     auto walk_quarter = [&]<int qi>() __attribute__((always_inline)) {   // steps qi*Q+Q-1 .. qi*Q
 #pragma unroll
       for (int i = Q - 1; i >= 0; --i) {
-        const u32x4 lo = dw[qi & 1][i][0], hi = dw[qi & 1][i][1];
-        const uint32_t st = (uint32_t)h;
-        const uint32_t m5 = (uint32_t)__builtin_amdgcn_sbfe((int)st, 5, 1);   // 0 / -1 per state bit
-        const uint32_t m6 = (uint32_t)__builtin_amdgcn_sbfe((int)st, 6, 1);
-        const uint32_t m7 = (uint32_t)__builtin_amdgcn_sbfe((int)st, 7, 1);
-        const uint32_t l0 = select_v(m5, lo.y, lo.x), l1 = select_v(m5, lo.w, lo.z);
-        const uint32_t l2 = select_v(m5, hi.y, hi.x), l3 = select_v(m5, hi.w, hi.z);
-        const uint32_t k0 = select_v(m6, l1, l0), k1 = select_v(m6, l3, l2);
-        const uint32_t word = select_v(m7, k1, k0);
-        const uint32_t dbit = __builtin_amdgcn_ubfe(word, st & 31u, 1);
+        const uint32_t* w = dw[qi & 1][i];
+        const uint32_t st = (uint32_t)h & (S - 1);
+        // where the state's decision sits: (word << 5) | bit (packed: the LDS table; AB & 32: skip it)
+        const uint32_t pos = (PACK && (ABLATE & 32) == 0) ? reinterpret_cast<const uint8_t*>(ptab)[st] : st;
+        const uint32_t m5 = (uint32_t)__builtin_amdgcn_sbfe((int)pos, 5, 1);   // 0 / -1 per word-index bit
+        const uint32_t m6 = (uint32_t)__builtin_amdgcn_sbfe((int)pos, 6, 1);
+        const uint32_t m7 = (uint32_t)__builtin_amdgcn_sbfe((int)pos, 7, 1);
+        const uint32_t l0 = select_v(m5, w[1], w[0]), l1 = select_v(m5, w[3], w[2]);
+        const uint32_t l2 = select_v(m5, w[W > 5 ? 5 : 4], w[4]);
+        const uint32_t k0 = select_v(m6, l1, l0);
+        uint32_t word;
+        if constexpr (W == 6) {
+          word = select_v(m7, l2, k0);   // words 4, 5: bit 7 set, bit 6 clear
+        } else {
+          const uint32_t l3 = select_v(m5, w[W > 7 ? 7 : 4], w[W > 6 ? 6 : 4]);
+          word = select_v(m7, select_v(m6, l3, l2), k0);
+        }
+        const uint32_t dbit = __builtin_amdgcn_ubfe(word, pos & 31u, 1);
         h = (h << 1) | dbit;
       }
     };

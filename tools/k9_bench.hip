@@ -56,16 +56,16 @@ double run(const char* name, RegArgs a, int ngroups, int cus) {
 }
 
 // the one-lane-per-block kernel (acs_wide.hpp), decisions in a per-wave global scratch slot
-template <int AB = 0>
+template <int AB = 0, bool PACK = false>
 double run_wide(const char* name, RegArgs a, int ngroups, int cus) {
-  auto kern = viterbi_wide_persist<kK9, 40, AB>;
+  auto kern = viterbi_wide_persist<kK9, 40, AB, PACK>;
   ngroups = (a.nblocks + 63) / 64;   // 64-block groups (one lane per block)
   int per_cu = 0;
   CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
   if (per_cu >= 4) per_cu -= per_cu % 4;
   const int grid = per_cu * cus < ngroups ? per_cu * cus : ngroups;
   static void* scratch = nullptr;
-  if (!scratch) CHECK(hipMalloc(&scratch, (size_t)grid * wide_slot_bytes(40)));
+  if (!scratch) CHECK(hipMalloc(&scratch, (size_t)grid * wide_slot_bytes<kK9>(40)));
   a.dec = scratch;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -180,12 +180,12 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 2; ++k) printf("  %-26s %.4f ms  %.3f\n", names[k], med(t[k]), med(t[k]) / med(t[0]));
     {
       std::vector<std::vector<double>> tw(4);
-      const char* wn[4] = {"wide", "wide, input default policy", "wide, stores drained first", "wide, no traceback loads"};
+      const char* wn[4] = {"wide (8 words per step)", "packed 6 words, LDS position table", "packed, no table (wrong output)", "packed ACS, hi words stored as dwordx4"};
       for (int round = 0; round < 5; ++round) {
         tw[0].push_back(run_wide<0>(wn[0], c, ngroups, cus)); check();
-        tw[1].push_back(run_wide<4>(wn[1], c, ngroups, cus)); check();
-        tw[2].push_back(run_wide<16>(wn[2], c, ngroups, cus)); check();
-        tw[3].push_back(run_wide<2>(wn[3], c, ngroups, cus));
+        tw[1].push_back(run_wide<0, true>(wn[1], c, ngroups, cus)); check();
+        tw[2].push_back(run_wide<32, true>(wn[2], c, ngroups, cus));
+        tw[3].push_back(run_wide<64, true>(wn[3], c, ngroups, cus)); check();
       }
       for (int k = 0; k < 4; ++k) printf("  %-26s %.4f ms  %.3f\n", wn[k], med(tw[k]), med(tw[k]) / med(tw[0]));
     }
