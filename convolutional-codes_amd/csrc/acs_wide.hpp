@@ -20,6 +20,7 @@
 #include <utility>
 
 #include "acs_persist.hpp"
+#include "k9_twins.hpp"
 
 namespace ccv {
 
@@ -38,9 +39,9 @@ constexpr uint32_t collapsed_mask_word(int w) {
   return m;
 }
 
-// Packed decisions (PACK): a collapsed butterfly's upper decision IS its lower one (same candidates
-// by construction), so only the lower words and the non-collapsed upper decisions are stored,
-// densely: K = 9 idiom 128 + 43 bits = 6 words per step instead of 8.
+// Packed decisions (PACK 1): a collapsed butterfly's upper decision IS its lower one (same
+// candidates by construction), so only the lower words and the non-collapsed upper decisions are
+// stored, densely: K = 9 idiom 128 + 43 bits = 6 words per step instead of 8.
 template <CodeSpec C>
 constexpr int noncollapsed_count() {
   int n = 0;
@@ -57,6 +58,19 @@ template <CodeSpec C>
 constexpr int packed_words() {
   return (1 << (C.K - 2)) / 32 + (noncollapsed_count<C>() + 31) / 32;
 }
+// PACK 2: one decision per value-numbering class of the K = 9 idiom trellis (k9_twins.hpp, generated)
+template <CodeSpec C>
+constexpr bool twin_code() {
+  return C.K == 9 && C.n == 2 && C.gen == GEN_REF_X86 && C.poly[0] == kK9TwinPolys[0] &&
+         C.poly[1] == kK9TwinPolys[1];
+}
+struct TwinPosTable {
+  uint32_t v[64];
+  constexpr TwinPosTable() : v() {
+    for (int s = 0; s < 256; ++s) v[s / 4] |= (uint32_t)kK9TwinPos[s] << (8 * (s % 4));
+  }
+};
+
 template <CodeSpec C>
 struct PackedPosTable {
   uint32_t v[(1 << (C.K - 1)) / 4];   // four 8-bit positions (word << 5 | bit) per word
@@ -91,7 +105,7 @@ __device__ __forceinline__ uint32_t select_v(uint32_t m, uint32_t a, uint32_t b)
 // One trellis step over S = 2^(K-1) > 64 states in one lane: decision word w holds new states
 // 32w .. 32w + 31 (bit k = state 32w + k). Butterfly j (old 2j, 2j+1 -> new j, j + S/2) as acs_step;
 // a collapsed butterfly's upper decision is the lower one's, filled per word by one v_bitop3.
-template <CodeSpec C, bool PACK, int NW>
+template <CodeSpec C, int PACK, int NW>
 __device__ __forceinline__ void acs_step_wide(float (&M)[1 << (C.K - 1)], const float (&BM)[1 << C.n],
                                               uint32_t (&d)[NW]) {
   constexpr int S = 1 << (C.K - 1);
@@ -108,9 +122,15 @@ __device__ __forceinline__ void acs_step_wide(float (&M)[1 << (C.K - 1)], const 
       const float b0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 1)];
       const float b1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 1)];
       N[j] = vmin(a0, a1);
-      d[j / 32] = shift_in(d[j / 32], a0, a1);
       N[j + H] = vmin(b0, b1);
-      if constexpr (PACK && !collapsed_butterfly<C>(j)) {
+      if constexpr (PACK == 2) {   // the class representatives only, at their packed positions
+        if constexpr (kK9TwinRep[j] != 0) d[kK9TwinPos[j] >> 5] = shift_in(d[kK9TwinPos[j] >> 5], a0, a1);
+        if constexpr (kK9TwinRep[j + H] != 0)
+          d[kK9TwinPos[j + H] >> 5] = shift_in(d[kK9TwinPos[j + H] >> 5], b0, b1);
+        return;
+      }
+      d[j / 32] = shift_in(d[j / 32], a0, a1);
+      if constexpr (PACK == 1 && !collapsed_butterfly<C>(j)) {
         constexpr int w = HW + noncollapsed_rank<C>(j) / 32;
         d[w] = shift_in(d[w], b0, b1);
       } else if constexpr (!collapsed_butterfly<C>(j)) {
@@ -171,9 +191,11 @@ __device__ __forceinline__ uint32_t argmin_wide(const float (&M)[S]) {
 
 // Scratch: one slot per wave of the grid, [main step][half][lane][4 words] (a store of four words of
 // 64 lanes is one contiguous KiB).
-template <CodeSpec C, bool PACK>
-constexpr int wide_words() { return PACK ? packed_words<C>() : (1 << (C.K - 1)) / 32; }
-template <CodeSpec C, bool PACK = false>
+template <CodeSpec C, int PACK>
+constexpr int wide_words() {
+  return PACK == 2 ? kK9TwinWords : PACK == 1 ? packed_words<C>() : (1 << (C.K - 1)) / 32;
+}
+template <CodeSpec C, int PACK = 0>
 constexpr size_t wide_slot_bytes(int main_steps) {
   return (size_t)main_steps * kRegThreads * 4 * wide_words<C, PACK>();
 }
@@ -181,10 +203,12 @@ constexpr size_t wide_slot_bytes(int main_steps) {
 // ABLATE (timing studies, tools/k9_bench.hip; production 0): 1 decisions discarded, 2 no traceback
 // loads, 4 input with the default cache policy, 16 drain the decision stores before the traceback,
 // 32 packed without the position table (wrong output), 64 packed upper words padded to a dwordx4.
-// PACK (production: true): 6 decision words per step -- the 128 lower ones and the 43 non-collapsed
-// upper ones dense, a state's (word, bit) from a 256-byte LDS table in the traceback -- instead of 8
-// with the collapsed upper bits filled in: 0.90x the time (profiles/r03_k9_wide_packed_ab.txt).
-template <CodeSpec C, int BLEN, int ABLATE = 0, bool PACK = false>
+// PACK: decision words per step. 0: 8, the collapsed upper bits filled in from the lower words;
+// 1: 6, the 128 lower decisions and the 43 non-collapsed upper ones dense (0.91x the time of 0);
+// 2 (production): 5, one per value-numbering class of the trellis (156, k9_twins.hpp; 0.87x). With
+// 1 and 2 the traceback takes a state's (word, bit) from a 256-byte LDS table
+// (profiles/r03_k9_wide_packed_ab.txt, profiles/r03_k9_wide_twin_ab.txt).
+template <CodeSpec C, int BLEN, int ABLATE = 0, int PACK = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void viterbi_wide_persist(RegArgs a, int ngroups) {
   constexpr int S = 1 << (C.K - 1);
@@ -200,7 +224,8 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
   constexpr int W = wide_words<C, PACK>();    // decision words per step
   constexpr int WH = W - 4;                   // upper words
-  static_assert(WH == 2 || WH == 4, "upper words stored as one dwordx2 / dwordx4 per lane");
+  static_assert(WH == 1 || WH == 2 || WH == 4, "upper words stored as one dword / dwordx2 / dwordx4 per lane");
+  static_assert(PACK != 2 || twin_code<C>(), "k9_twins.hpp describes the K = 9 (561,753) x86-idiom code");
   constexpr int WS = (ABLATE & 64) ? 4 : WH;  // upper words as stored (AB & 64: padded to a dwordx4)
   constexpr int STEPB = kRegThreads * 4 * (4 + WS);   // slot bytes per main step
   static_assert(T % PF == 0 && G == PF, "K = 9 at blen 40: chunk 0 is the growth, 5 main chunks");
@@ -255,8 +280,11 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   __shared__ uint32_t ptab[PACK ? S / 4 : 1];
-  if constexpr (PACK) {
+  if constexpr (PACK == 1) {
     static constexpr PackedPosTable<C> kPos{};
+    ptab[lane] = kPos.v[lane];
+  } else if constexpr (PACK == 2) {
+    static constexpr TwinPosTable kPos{};
     ptab[lane] = kPos.v[lane];
   }
 
@@ -302,7 +330,9 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
             asm volatile("" ::"v"(x));
           } else {
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[0], d[1], d[2], d[3]}, slot, col, m * STEPB, 0);
-            if constexpr (WS == 2)
+            if constexpr (WS == 1)
+              __builtin_amdgcn_raw_buffer_store_b32(d[4], slot, colh, m * STEPB + 1024, 0);
+            else if constexpr (WS == 2)
               __builtin_amdgcn_raw_buffer_store_b64(u32x2{d[4], d[W > 5 ? 5 : 4]}, slot, colh, m * STEPB + 1024, 0);
             else
               __builtin_amdgcn_raw_buffer_store_b128(u32x4{d[4], d[W > 5 ? 5 : 4], d[W > 6 ? 6 : 4], d[W > 7 ? 7 : 4]},
@@ -344,12 +374,15 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
         } else {
           const int m = qi * Q + i;
           lo = __builtin_amdgcn_raw_buffer_load_b128(slot, col, m * STEPB, 0);
-          if constexpr (WS == 2) hi2 = __builtin_amdgcn_raw_buffer_load_b64(slot, colh, m * STEPB + 1024, 0);
+          if constexpr (WS == 1) hi2 = u32x2{__builtin_amdgcn_raw_buffer_load_b32(slot, colh, m * STEPB + 1024, 0), 0u};
+          else if constexpr (WS == 2) hi2 = __builtin_amdgcn_raw_buffer_load_b64(slot, colh, m * STEPB + 1024, 0);
           else hi4 = __builtin_amdgcn_raw_buffer_load_b128(slot, colh, m * STEPB + 1024, 0);
           if constexpr (WS == 4 && WH == 2) hi2 = u32x2{hi4.x, hi4.y};
         }
         dw[qi & 1][i][0] = lo.x; dw[qi & 1][i][1] = lo.y; dw[qi & 1][i][2] = lo.z; dw[qi & 1][i][3] = lo.w;
-        if constexpr (WH == 2) {
+        if constexpr (WH == 1) {
+          dw[qi & 1][i][4] = hi2.x;
+        } else if constexpr (WH == 2) {
           dw[qi & 1][i][4] = hi2.x; dw[qi & 1][i][W > 5 ? 5 : 4] = hi2.y;
         } else {
           dw[qi & 1][i][4] = hi4.x; dw[qi & 1][i][W > 5 ? 5 : 4] = hi4.y;
@@ -371,7 +404,9 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
         const uint32_t l2 = select_v(m5, w[W > 5 ? 5 : 4], w[4]);
         const uint32_t k0 = select_v(m6, l1, l0);
         uint32_t word;
-        if constexpr (W == 6) {
+        if constexpr (W == 5) {
+          word = select_v(m7, w[4], k0);   // word 4: bit 7 set, bits 5, 6 clear
+        } else if constexpr (W == 6) {
           word = select_v(m7, l2, k0);   // words 4, 5: bit 7 set, bit 6 clear
         } else {
           const uint32_t l3 = select_v(m5, w[W > 7 ? 7 : 4], w[W > 6 ? 6 : 4]);

@@ -52,11 +52,11 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence
 
 template <size_t I>
 hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
-  // one lane per block, packed decisions through a per-wave scratch slot: ~0.6x the time of the
-  // four-lane kernel below at 32 frames, bit-identical (tools/k9_bench.hip, profiles/r03_k9_wide.txt,
-  // profiles/r03_k9_wide_packed_ab.txt)
+  // one lane per block, one decision per value-numbering class (156 of 256 states, k9_twins.hpp)
+  // through a per-wave scratch slot: ~0.57x the time of the four-lane kernel below at 32 frames,
+  // bit-identical (tools/k9_bench.hip, profiles/r03_k9_wide*.txt)
   if constexpr (kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2 && kMultiCodes[I].gen == GEN_REF_X86)
-    return launch_persistent(viterbi_wide_persist<kMultiCodes[I], kPersistBlen, 0, true>, a, ngroups, stream);
+    return launch_persistent(viterbi_wide_persist<kMultiCodes[I], kPersistBlen, 0, 2>, a, ngroups, stream);
   else
     return hipErrorInvalidValue;
 }
@@ -83,7 +83,7 @@ const RegLaunchFn* multi_persist_launchers() { return kSoftPersist.data(); }
 
 const RegLaunchFn* multi_wide_launchers() { return kSoftWide.data(); }
 
-size_t multi_wide_slot_bytes() { return wide_slot_bytes<kMultiCodes[2], true>(kPersistBlen); }
+size_t multi_wide_slot_bytes() { return wide_slot_bytes<kMultiCodes[2], 2>(kPersistBlen); }
 
 const RegLaunchFn* multi_regdec_launchers(bool hard) {
   return hard ? kHardRegDec.data() : kSoftRegDec.data();

@@ -56,7 +56,7 @@ double run(const char* name, RegArgs a, int ngroups, int cus) {
 }
 
 // the one-lane-per-block kernel (acs_wide.hpp), decisions in a per-wave global scratch slot
-template <int AB = 0, bool PACK = false>
+template <int AB = 0, int PACK = 0>
 double run_wide(const char* name, RegArgs a, int ngroups, int cus) {
   auto kern = viterbi_wide_persist<kK9, 40, AB, PACK>;
   ngroups = (a.nblocks + 63) / 64;   // 64-block groups (one lane per block)
@@ -180,12 +180,12 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 2; ++k) printf("  %-26s %.4f ms  %.3f\n", names[k], med(t[k]), med(t[k]) / med(t[0]));
     {
       std::vector<std::vector<double>> tw(4);
-      const char* wn[4] = {"wide (8 words per step)", "packed 6 words, LDS position table", "packed, no table (wrong output)", "packed ACS, hi words stored as dwordx4"};
+      const char* wn[4] = {"wide (8 words per step)", "packed 6 words (collapsed butterflies)", "5 words, one per twin class", "5 words, no table (wrong output)"};
       for (int round = 0; round < 5; ++round) {
         tw[0].push_back(run_wide<0>(wn[0], c, ngroups, cus)); check();
-        tw[1].push_back(run_wide<0, true>(wn[1], c, ngroups, cus)); check();
-        tw[2].push_back(run_wide<32, true>(wn[2], c, ngroups, cus));
-        tw[3].push_back(run_wide<64, true>(wn[3], c, ngroups, cus)); check();
+        tw[1].push_back(run_wide<0, 1>(wn[1], c, ngroups, cus)); check();
+        tw[2].push_back(run_wide<0, 2>(wn[2], c, ngroups, cus)); check();
+        tw[3].push_back(run_wide<32, 2>(wn[3], c, ngroups, cus));
       }
       for (int k = 0; k < 4; ++k) printf("  %-26s %.4f ms  %.3f\n", wn[k], med(tw[k]), med(tw[k]) / med(tw[0]));
     }
