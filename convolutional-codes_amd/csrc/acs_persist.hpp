@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "acs_reg.hpp"
+#include "twins.hpp"
 
 namespace ccv {
 
@@ -149,6 +150,71 @@ __device__ __forceinline__ uint64_t traceback_regs(const DW (&D)[F], uint32_t st
   return __builtin_bitreverse64(H);   // bit 63 - t = output of step t
 }
 
+// One stored decision per value-numbering class (twins.hpp, generated by tools/gen_twins.py) for the
+// x86-idiom K = 7 / K = 9 codes: states whose candidate pairs are the same expressions share their
+// decision at every main step, so only each class's first state in processing order (butterfly j
+// descending, state j then j + S/2) shifts its decision in, at the class's position.
+template <CodeSpec C>
+constexpr bool twin_code() {
+  if constexpr (C.K == 7 || C.K == 9)
+    return C.n == 2 && C.gen == GEN_REF_X86 && C.poly[0] == TwinTable<C.K>::polys[0] &&
+           C.poly[1] == TwinTable<C.K>::polys[1];
+  else
+    return false;
+}
+
+// acs_step (soft, fp32) with the class layout, S <= 64: the 39 classes of K = 7 in 2 words.
+template <CodeSpec C>
+__device__ __forceinline__ uint64_t acs_step_twin(float (&M)[1 << (C.K - 1)], const float (&BM)[1 << C.n]) {
+  constexpr int S = 1 << (C.K - 1);
+  constexpr int H = S / 2;
+  using TT = TwinTable<C.K>;
+  static_assert(TT::words == 2, "two decision words per step");
+  float N[S];
+  uint32_t d[2] = {0u, 0u};
+  [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
+    ([&]() __attribute__((always_inline)) {
+      constexpr int j = H - 1 - js;
+      const float a0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 0)];
+      const float a1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 0)];
+      const float b0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 1)];
+      const float b1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 1)];
+      N[j] = vmin(a0, a1);
+      N[j + H] = vmin(b0, b1);
+      if constexpr (TT::rep[j] != 0) d[TT::pos[j] >> 5] = shift_in(d[TT::pos[j] >> 5], a0, a1);
+      if constexpr (TT::rep[j + H] != 0) d[TT::pos[j + H] >> 5] = shift_in(d[TT::pos[j + H] >> 5], b0, b1);
+    }(), ...);
+  }(std::make_integer_sequence<int, H>{});
+#pragma unroll
+  for (int s = 0; s < S; ++s) M[s] = N[s];
+  return ((uint64_t)d[1] << 32) | d[0];
+}
+
+// traceback_regs with the class layout: a state's decision bit comes from the LDS position table.
+template <int K, int F>
+__device__ __forceinline__ uint64_t traceback_twin(const uint64_t (&D)[F], uint32_t st, int F_rt,
+                                                   const uint8_t* pos) {
+  constexpr int S = 1 << (K - 1);
+  constexpr int T = F + K - 1;
+  static_assert(T <= 64, "history fits two words");
+  constexpr int SPLIT = 33 - K;
+  uint32_t h = st, hi = 0;
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    const int m = F - 1 - j;
+    if (m % 8 == 7 || m == F - 1) {
+      if (m >= F_rt) continue;
+    }
+    const uint32_t d = (uint32_t)(D[m] >> pos[h & (S - 1)]);
+    h = (h << 1) | (d & 1u);
+    if (j + 1 == SPLIT) hi = h;
+  }
+  uint64_t H;
+  if constexpr (F <= SPLIT) H = h;
+  else H = ((uint64_t)hi << (F - SPLIT)) | (h & ((1u << (F - SPLIT)) - 1u));
+  return __builtin_bitreverse64(H);
+}
+
 // Output bytes (MSB-first, reference traceback :88) and the bit errors of the first blen bits
 // against the transmitted info bytes (consumer AWGN-channel/main.c:118-144). Static sizes: runtime
 // byte loops here cost the persistent kernels their register allocation (spills).
@@ -207,7 +273,7 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
              kPersistDepth2 = 16, kPersistLineChunks = 32, kPersistNoMemRandom = 64,
-             kPersistNoDma = 128, kPersistNoLdsRead = 256, kPersistInputNt = 512 };
+             kPersistNoDma = 128, kPersistNoLdsRead = 256, kPersistInputNt = 512, kPersistTwins = 1024 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -244,6 +310,19 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
 
   __shared__ __attribute__((aligned(1024))) unsigned char
       lds[(LINES || DEPTH2) ? 2 * BUF : BUF];
+  // kPersistTwins (A/B, not the production path): one decision per value-numbering class of the
+  // x86-idiom K = 7 code (twins.hpp) -- 3.7 % fewer VALU, but the traceback's state -> (word, bit)
+  // lookup in LDS lengthens its dependent chain: 1.02x the time (profiles/r03_k7_twin_ab.txt)
+  constexpr bool TWINS = twin_code<C>() && (ABLATE & kPersistTwins) != 0 && S == 64;
+  __shared__ uint32_t twin_pos[TWINS ? S / 4 : 1];
+  if constexpr (TWINS) {
+    if (lane < S / 4) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v |= (uint32_t)TwinTable<C.K>::pos[4 * lane + k] << (8 * k);
+      twin_pos[lane] = v;
+    }
+  }
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   constexpr uint32_t block_bytes = (uint32_t)T * 16;
   // DMA k of a chunk: lane l moves 16-byte unit j = l % 8 of block r = 8k + l / 8 of the group, from
@@ -435,6 +514,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
         if constexpr (t < G) growth_step<C, t, float>(M, bm, __builtin_inff());
         else if constexpr (t < T) {
           if constexpr ((ABLATE & kPersistSelectAcs) != 0) D[t - G] = acs_step_select<C>(M, bm);
+          else if constexpr (TWINS) D[t - G] = acs_step_twin<C>(M, bm);
           else D[t - G] = acs_step<C, false, float>(M, bm);
           pin(D[t - G]);
         }
@@ -458,7 +538,9 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
     } else {
       float best;
       const uint32_t st = (uint32_t)argmin_state<S, float>(M, __builtin_inff(), best);
-      const uint64_t bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
+      uint64_t bits;
+      if constexpr (TWINS) bits = traceback_twin<C.K, BLEN>(D, st, a.blen, reinterpret_cast<const uint8_t*>(twin_pos));
+      else bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
       uint64_t ref = 0;
 #pragma unroll
       for (int k = 0; k < IB; ++k) ref |= (uint64_t)info[k] << (56 - 8 * k);

@@ -20,7 +20,7 @@
 #include <utility>
 
 #include "acs_persist.hpp"
-#include "k9_twins.hpp"
+#include "twins.hpp"
 
 namespace ccv {
 
@@ -58,16 +58,14 @@ template <CodeSpec C>
 constexpr int packed_words() {
   return (1 << (C.K - 2)) / 32 + (noncollapsed_count<C>() + 31) / 32;
 }
-// PACK 2: one decision per value-numbering class of the K = 9 idiom trellis (k9_twins.hpp, generated)
-template <CodeSpec C>
-constexpr bool twin_code() {
-  return C.K == 9 && C.n == 2 && C.gen == GEN_REF_X86 && C.poly[0] == kK9TwinPolys[0] &&
-         C.poly[1] == kK9TwinPolys[1];
-}
+// PACK 2: one decision per value-numbering class of the idiom trellis (twins.hpp, generated)
+// (twin_code: acs_persist.hpp)
+// four 8-bit positions per word, for an LDS copy
+template <int K>
 struct TwinPosTable {
-  uint32_t v[64];
+  uint32_t v[(1 << (K - 1)) / 4];
   constexpr TwinPosTable() : v() {
-    for (int s = 0; s < 256; ++s) v[s / 4] |= (uint32_t)kK9TwinPos[s] << (8 * (s % 4));
+    for (int s = 0; s < (1 << (K - 1)); ++s) v[s / 4] |= (uint32_t)TwinTable<K>::pos[s] << (8 * (s % 4));
   }
 };
 
@@ -124,9 +122,9 @@ __device__ __forceinline__ void acs_step_wide(float (&M)[1 << (C.K - 1)], const 
       N[j] = vmin(a0, a1);
       N[j + H] = vmin(b0, b1);
       if constexpr (PACK == 2) {   // the class representatives only, at their packed positions
-        if constexpr (kK9TwinRep[j] != 0) d[kK9TwinPos[j] >> 5] = shift_in(d[kK9TwinPos[j] >> 5], a0, a1);
-        if constexpr (kK9TwinRep[j + H] != 0)
-          d[kK9TwinPos[j + H] >> 5] = shift_in(d[kK9TwinPos[j + H] >> 5], b0, b1);
+        using TT = TwinTable<C.K>;
+        if constexpr (TT::rep[j] != 0) d[TT::pos[j] >> 5] = shift_in(d[TT::pos[j] >> 5], a0, a1);
+        if constexpr (TT::rep[j + H] != 0) d[TT::pos[j + H] >> 5] = shift_in(d[TT::pos[j + H] >> 5], b0, b1);
         return;
       }
       d[j / 32] = shift_in(d[j / 32], a0, a1);
@@ -193,7 +191,8 @@ __device__ __forceinline__ uint32_t argmin_wide(const float (&M)[S]) {
 // 64 lanes is one contiguous KiB).
 template <CodeSpec C, int PACK>
 constexpr int wide_words() {
-  return PACK == 2 ? kK9TwinWords : PACK == 1 ? packed_words<C>() : (1 << (C.K - 1)) / 32;
+  if constexpr (PACK == 2) return TwinTable<C.K>::words;
+  else return PACK == 1 ? packed_words<C>() : (1 << (C.K - 1)) / 32;
 }
 template <CodeSpec C, int PACK = 0>
 constexpr size_t wide_slot_bytes(int main_steps) {
@@ -205,7 +204,7 @@ constexpr size_t wide_slot_bytes(int main_steps) {
 // 32 packed without the position table (wrong output), 64 packed upper words padded to a dwordx4.
 // PACK: decision words per step. 0: 8, the collapsed upper bits filled in from the lower words;
 // 1: 6, the 128 lower decisions and the 43 non-collapsed upper ones dense (0.91x the time of 0);
-// 2 (production): 5, one per value-numbering class of the trellis (156, k9_twins.hpp; 0.87x). With
+// 2 (production): 5, one per value-numbering class of the trellis (156, twins.hpp; 0.87x). With
 // 1 and 2 the traceback takes a state's (word, bit) from a 256-byte LDS table
 // (profiles/r03_k9_wide_packed_ab.txt, profiles/r03_k9_wide_twin_ab.txt).
 template <CodeSpec C, int BLEN, int ABLATE = 0, int PACK = 0>
@@ -225,7 +224,7 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   constexpr int W = wide_words<C, PACK>();    // decision words per step
   constexpr int WH = W - 4;                   // upper words
   static_assert(WH == 1 || WH == 2 || WH == 4, "upper words stored as one dword / dwordx2 / dwordx4 per lane");
-  static_assert(PACK != 2 || twin_code<C>(), "k9_twins.hpp describes the K = 9 (561,753) x86-idiom code");
+  static_assert(PACK != 2 || twin_code<C>(), "twins.hpp describes the K = 9 (561,753) x86-idiom code");
   constexpr int WS = (ABLATE & 64) ? 4 : WH;  // upper words as stored (AB & 64: padded to a dwordx4)
   constexpr int STEPB = kRegThreads * 4 * (4 + WS);   // slot bytes per main step
   static_assert(T % PF == 0 && G == PF, "K = 9 at blen 40: chunk 0 is the growth, 5 main chunks");
@@ -284,7 +283,7 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
     static constexpr PackedPosTable<C> kPos{};
     ptab[lane] = kPos.v[lane];
   } else if constexpr (PACK == 2) {
-    static constexpr TwinPosTable kPos{};
+    static constexpr TwinPosTable<C.K> kPos{};
     ptab[lane] = kPos.v[lane];
   }
 

@@ -52,7 +52,7 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence
 
 template <size_t I>
 hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
-  // one lane per block, one decision per value-numbering class (156 of 256 states, k9_twins.hpp)
+  // one lane per block, one decision per value-numbering class (156 of 256 states, twins.hpp)
   // through a per-wave scratch slot: ~0.57x the time of the four-lane kernel below at 32 frames,
   // bit-identical (tools/k9_bench.hip, profiles/r03_k9_wide*.txt)
   if constexpr (kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2 && kMultiCodes[I].gen == GEN_REF_X86)

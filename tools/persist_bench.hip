@@ -119,6 +119,7 @@ int ab(RegArgs a, int ng, int cus, bool only_first = false) {
   auto A = [&]() { return sustained<kK7Ref, 0>(a, ng, 8, cus, 40); };
   struct V { const char* name; float (*f)(RegArgs, int, int, int, int); bool b42; };
   const V vs_all[] = {
+    {"twin classes (one decision per class)", sustained<kK7Ref, kPersistTwins>, false},
     {"input nt (aux 2)", sustained<kK7Ref, kPersistInputNt>, false},
     {"2-deep DMA", sustained<kK7Ref, kPersistDepth2>, false},
     {"no DMA (stale LDS rows)", sustained<kK7Ref, kPersistNoDma>, false},
@@ -231,7 +232,7 @@ int main(int argc, char** argv) {
   a.out = d_out;
   const int ng = nb / 64;
   if (argc > 1 && std::string(argv[1]) == "ab") return ab(a, ng, cus);
-  if (argc > 1 && std::string(argv[1]) == "abnt") return ab(a, ng, cus, true);   // input nt only
+  if (argc > 1 && std::string(argv[1]) == "abtw") return ab(a, ng, cus, true);   // twin classes only
   if (argc > 1 && std::string(argv[1]) == "abh") return ab_hard<1>(cus) | ab_hard<2>(cus);
   if (argc > 1) {   // persist_bench trace [launches]
     const int n = argc > 2 ? atoi(argv[2]) : 300;
