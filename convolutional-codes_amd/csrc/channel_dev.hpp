@@ -430,24 +430,43 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
 }
 
 // Frames only: one lane per block draws its info bytes and its whole decoder input and writes them
-// to a.info_out / a.ch_out (soft float [nb][T][2^n], 16-byte row stores at n = 2); no decode. The
-// K = 9 sweep decodes these frames with the one-lane-per-block kernel (acs_wide.hpp) instead of
-// running the channel once per lane of a block's four-lane group (viterbi_channel_multi below).
+// to a.info_out / a.ch_out (soft float [nb][T][2^n] at n = 2); no decode. The K = 9 sweep decodes
+// these frames with the one-lane-per-block kernel (acs_wide.hpp) instead of running the channel once
+// per lane of a block's four-lane group (viterbi_channel_multi below).
+// Rows go out through LDS, 8 steps at a time: lane-per-row 16-byte stores put one wave's 64 stores
+// in 64 different 128-byte lines, which L2 evicts half-written (WRITE_SIZE 2.5x the frame bytes,
+// DESIGN.md 4.4); staged, store instruction j writes rows 8j .. 8j+7, 8 lanes per 128-byte line.
 template <CodeSpec C, bool HARD>
 __global__ __launch_bounds__(kRegThreads) void channel_frames(ChanArgs a) {
   static_assert(!HARD && C.n == 2, "soft r = 1/2 frames");
   using Src = ChannelSource<C, HARD>;
-  const int b = blockIdx.x * kRegThreads + threadIdx.x;
-  if (b >= a.r.nblocks) return;
+  constexpr int CH = 8;   // steps per staged chunk: CH x 16 B = one 128-byte line of a row
+  __shared__ float4 stage[CH][kRegThreads];
+  const int lane = threadIdx.x;
+  const int b0 = blockIdx.x * kRegThreads;
+  const int nb = a.r.nblocks, T = a.r.T;
+  const int b = b0 + lane;
   Src src;
-  src.init(a, b, true);
-  src.out = nullptr;   // rows are stored here as one 16-byte store each
-  float4* row = reinterpret_cast<float4*>(a.ch_out) + (size_t)b * a.r.T;
+  src.init(a, b < nb ? b : nb - 1, b < nb);   // every lane runs: the stores below are cooperative
+  src.out = nullptr;
+  const int sub = lane & (CH - 1), rsub = lane / CH;
+  float4* frame = reinterpret_cast<float4*>(a.ch_out);
 #pragma unroll 1
-  for (int t = 0; t < a.r.T; ++t) {
-    float BM[4];
-    src.next(BM);
-    row[t] = float4{BM[0], BM[1], BM[2], BM[3]};
+  for (int c0 = 0; c0 < T; c0 += CH) {
+    const int n = T - c0 < CH ? T - c0 : CH;
+#pragma unroll 1
+    for (int k = 0; k < n; ++k) {
+      float BM[4];
+      src.next(BM);
+      stage[k][lane] = float4{BM[0], BM[1], BM[2], BM[3]};
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int j = 0; j < kRegThreads / CH; ++j) {
+      const int r = j * CH + rsub;
+      if (sub < n && b0 + r < nb) frame[(size_t)(b0 + r) * T + c0 + sub] = stage[sub][r];
+    }
+    __syncthreads();
   }
 }
 
