@@ -82,15 +82,33 @@ def cpu_threads(info=None):
     return max(1, n)
 
 
+def reference_cannot_decode(code, decoder="viterbi"):
+    """Why the reference decoder cannot run this code, or None. Its Viterbi argmin counts states in a
+    uint8_t (`for (uint8_t i = 0; i < obj->num_states; ++i)`, AWGN-channel/viterbi-decoder.c:74,
+    binary-symmetric-channel/viterbi-decoder.c:78), so at 2^(K-1) >= 256 states (K >= 9) the loop never
+    ends: calling it would hang bench.py."""
+    if decoder == "viterbi" and code.K >= 9:
+        return (f"reference Viterbi not run: K={code.K} has {code.states} states and its uint8_t argmin "
+                "counter never reaches them (AWGN-channel/viterbi-decoder.c:74 loops forever)")
+    if code.gen_mode != 0:
+        return ("reference not run: compiled here it decodes the x86-idiom code of its generator-bit "
+                "expression (common/encoder.c:95-100, SURVEY.md 0.4), not the textbook true-parity code")
+    return None
+
+
 def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi", hard=False):
     """Reference decoder (oracle/_ref, compiled from the reference's own sources) on host cores,
     over a bounded sample of the SAME frames the GPU decodes; its output is checked against the GPU's.
-    Falls back to the oracle restatement ("port", one thread) where oracle/_ref was not built."""
+    Falls back to the oracle restatement ("port", one thread) where oracle/_ref was not built or the
+    reference cannot decode the code (K >= 9, reference_cannot_decode)."""
     stack = decoder == "stack"
     suffix = "" if decoder == "viterbi" else "_" + decoder
     ref_so = os.path.join(REPO, "oracle", "_ref", f"libccref_{'bsc' if hard else 'awgn'}{suffix}.so")
     polys = (ctypes.c_uint64 * code.n)(*code.polys)
-    if os.path.exists(ref_so):
+    skipped = reference_cannot_decode(code, decoder)
+    if not os.path.exists(ref_so) and skipped is None:
+        skipped = f"{os.path.relpath(ref_so, REPO)} not built"
+    if skipped is None:
         lib = ctypes.CDLL(ref_so)
         if decoder != "viterbi":
             lib.ccref_set_stack_metrics.argtypes = [ctypes.c_float, ctypes.c_int32, ctypes.c_int32]
@@ -153,11 +171,16 @@ def cpu_baseline(code, rx, gpu_out, target_cpu_seconds, decoder="viterbi", hard=
         parity = diff <= starts
     bits = nb * code.blen
     host = host_cpu_info()
-    return {"value": round(bits / secs / 1e6, 4), "unit": "Mbit/s", "cores": threads, "kind": kind,
-            "sample": f"{nb} blocks ({bits} info bits) of the benchmark frames, {secs:.2f} s wall on "
-                      f"{threads} thread(s), one decoder_input() per trellis step as the reference "
-                      f"driver feeds it; output bit-identical to the GPU's: {parity}",
-            "bit_identical": parity, "host": host}, parity
+    how = ("one decoder_input() per trellis step as the reference driver feeds it" if kind == "reference"
+           else "oracle/ccoracle.c, the cited restatement of the reference decoder (same loop shape and "
+                "tie rules)")
+    res = {"value": round(bits / secs / 1e6, 4), "unit": "Mbit/s", "cores": threads, "kind": kind,
+           "sample": f"{nb} blocks ({bits} info bits) of the benchmark frames, {secs:.2f} s wall on "
+                     f"{threads} thread(s), {how}; output bit-identical to the GPU's: {parity}",
+           "bit_identical": parity, "host": host}
+    if skipped:
+        res["reference_skipped"] = skipped
+    return res, parity
 
 
 def cpu_optimized_baseline(code, rx, gpu_out, target_cpu_seconds, hard=False):
@@ -171,14 +194,27 @@ def cpu_optimized_baseline(code, rx, gpu_out, target_cpu_seconds, hard=False):
     res = O.fast_viterbi(oc, rx[:2000], hard=hard, threads=1)
     per_block = max(res[0] / 2000, 1e-8)
     nb = int(min(len(rx), max(threads * 2000, target_cpu_seconds * threads / per_block)))
-    res = O.fast_viterbi(oc, rx[:nb], hard=hard, threads=threads)
-    secs, out = res[0], res[1]
+    # one pass over the sample can be a fraction of a second at K <= 7 (2.6 M blocks ~ 0.1-0.2 s), so
+    # repeat passes until at least min_seconds of wall time and report the MEDIAN pass (a single short
+    # pass swung 2x between runs)
+    min_seconds, times, out = 2.0, [], None
+    while sum(times) < min_seconds or len(times) < 5:
+        res = O.fast_viterbi(oc, rx[:nb], hard=hard, threads=threads)
+        times.append(res[0])
+        if out is None:
+            out = res[1]
+        if len(times) >= 200:
+            break
+    secs = sorted(times)[len(times) // 2]
     parity = bool(np.array_equal(out, gpu_out[:nb]))
     bits = nb * code.blen
     return {"value": round(bits / secs / 1e6, 2), "unit": "Mbit/s", "cores": threads, "kind": "port",
-            "sample": f"{nb} blocks ({bits} info bits) of the benchmark frames, {secs:.2f} s wall on {threads} "
-                      f"thread(s): oracle/ccfast.c, table-driven ACS on 8/16 blocks per AVX2 vector; output "
-                      f"bit-identical to the GPU's: {parity}",
+            "sample": f"{nb} blocks ({bits} info bits) of the benchmark frames per pass, median of "
+                      f"{len(times)} passes ({sum(times):.2f} s wall in total; passes "
+                      f"{min(times):.3f}-{max(times):.3f} s) on {threads} thread(s): oracle/ccfast.c, "
+                      f"table-driven ACS on 8/16 blocks per AVX2 vector; output bit-identical to the GPU's: "
+                      f"{parity}",
+            "passes": len(times), "pass_seconds_median": round(secs, 4),
             "bit_identical": parity}
 
 

@@ -721,14 +721,15 @@ inline int resident_groups(Kern kernel, bool fresh = false) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kRegThreads, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  // CCV_PERSIST_WAVES_PER_CU caps the resident waves per CU (occupancy studies); read per kernel
+  // every wave walks the same number of groups: the same number of waves on each of a CU's four
+  // SIMDs, or the SIMDs holding one more wave finish a third later (10 per CU: 0.50 vs 0.39 ms)
+  if (per_cu >= 4) per_cu -= per_cu % 4;
+  // CCV_PERSIST_WAVES_PER_CU caps the resident waves per CU exactly (occupancy / L2 working-set
+  // studies, tools/waves_sweep.sh); read per kernel
   if (const char* env = std::getenv("CCV_PERSIST_WAVES_PER_CU")) {
     const int cap = std::atoi(env);
     if (cap > 0 && cap < per_cu) per_cu = cap;
   }
-  // every wave walks the same number of groups: the same number of waves on each of a CU's four
-  // SIMDs, or the SIMDs holding one more wave finish a third later (10 per CU: 0.50 vs 0.39 ms)
-  if (per_cu >= 4) per_cu -= per_cu % 4;
   if (!fresh) cache.entries.push_back({key, dev, per_cu * cus});
   return per_cu * cus;
 }

@@ -148,6 +148,58 @@ def test_reference_api_streaming(case):
     dec.destroy()
 
 
+@pytest.mark.parametrize("case", ["awgn_k7_4dB", "bsc_cb0_p100000"])
+def test_reference_api_callback_takes_ownership(case):
+    """A callback that returns 0 takes the output buffer (AWGN-channel/viterbi-decoder.c:92-106,
+    binary-symmetric-channel/viterbi-decoder.c:98-112; api_shim.cpp emit_output_buffer): the decoder
+    must allocate a fresh buffer for the next block and never touch the taken one again. Odd blocks
+    are taken (kept until the end, then freed with free() as the new owner), even blocks are copied
+    and handed back (-1), both through the streaming and the batch entry points: every taken buffer
+    still holds its own block, all taken pointers differ, and the handed-back blocks are correct."""
+    import ctypes
+    import ctypes.util
+    g = O.load_golden(case)
+    c = _code_of(g)
+    soft = case.startswith("awgn")
+    dec = SoftDecoder() if soft else HardDecoder()
+    dec.init(c)
+    taken, copied, pms = [], [], []
+    count = [0]
+
+    def take(data, length, *pm):
+        assert length == c.blen
+        count[0] += 1
+        if pm:
+            pms.append(int(pm[0]))
+        if count[0] % 2 == 1:
+            taken.append((count[0] - 1, ctypes.cast(data, ctypes.c_void_p).value))
+            return 0
+        copied.append((count[0] - 1, ctypes.string_at(data, c.out_bytes)))
+        return -1
+
+    from ccviterbi.decoder import _HARD_CB, _SOFT_CB
+    cb = (_SOFT_CB if soft else _HARD_CB)(take)
+    dec._lib.decoder_register_callback(dec._obj, ctypes.cast(cb, ctypes.c_void_p))
+    nb = 10
+    for b in range(nb):                                   # streaming: one step per call
+        for t in range(c.steps):
+            dec.input(g["rx"][b, t])
+    dec.input_blocks(g["rx"][nb:2 * nb])                  # batch extension, same callbacks
+    assert count[0] == 2 * nb
+    assert len({p for _, p in taken}) == len(taken) == nb, "a taken buffer was reused"
+    for b, p in taken:
+        assert ctypes.string_at(p, c.out_bytes) == g["out"][b].tobytes(), b
+    for b, data in copied:
+        assert data == g["out"][b].tobytes(), b
+    if not soft:
+        assert pms == [int(x) for x in g["path_metric"][:2 * nb]]
+    dec.destroy()
+    libc = ctypes.CDLL(ctypes.util.find_library("c"))
+    libc.free.argtypes = [ctypes.c_void_p]
+    for _, p in taken:
+        libc.free(p)
+
+
 def test_reference_api_generator_mode_true_parity():
     c = K7.with_(gen_mode=GEN_TRUE_PARITY)
     info, rx = ch.awgn_blocks(c, 300, ch.noise_scaling(3.0), 5)

@@ -26,7 +26,9 @@ run k7 300                                                     # config 2 (headl
 run k7_step 300 --layout step --no-cpu-baseline
 run bsc 300 --channel bsc                                      # config 4
 run code0_bsc 300 --code code0 --channel bsc                   # config 1 code at GPU scale
-run k9 300 --code k9 --frames 32 --no-cpu-baseline             # config 3
+run k9 300 --code k9 --frames 32                               # config 3 (port + AVX2 baselines)
+run k7_true 300 --code k7:true                                 # textbook (171,133)
+run k9_true 300 --code k9:true --frames 32                     # textbook (561,753)
 run stack 300 --decoder stack --frames 4 --steps 5 --warmup 1  # config 5
 run stack_bsc 300 --decoder stack --channel bsc --frames 4 --steps 5 --warmup 1
 run fano 600 --decoder fano --steps 3 --warmup 1 --no-cpu-baseline
