@@ -8,7 +8,9 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)            # convolutional-codes_amd/
-LIB_DIR = os.path.join(ROOT_DIR, "lib")
+# CCV_LIB_DIR: load another in-tree build of the same libraries instead (A/B timing of two builds in
+# one session, tools/ab_build.sh); still native code, never a fallback
+LIB_DIR = os.environ.get("CCV_LIB_DIR") or os.path.join(ROOT_DIR, "lib")
 
 _P = ctypes.POINTER
 _vp, _sz, _i, _u, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint, ctypes.c_uint64

@@ -22,6 +22,10 @@ FLAG_GLOBAL_DECISIONS = 4   # survivor decisions through an HBM scratch array (A
 FLAG_NO_PERSISTENT = 8      # skip the persistent K <= 7 kernels (A/B)
 
 
+CHANNEL_HARD_DEMAP = 1     # include/ccv.h CCV_CHANNEL_HARD_DEMAP
+CHANNEL_FRAMES_ONLY = 2    # include/ccv.h CCV_CHANNEL_FRAMES_ONLY
+
+
 class DecoderError(RuntimeError):
     pass
 
@@ -119,6 +123,18 @@ class Plan:
                                            _ptr(d_info), _ptr(d_out),
                                            _ptr(d_path_metric), _ptr(d_errors), _ptr(d_channel),
                                            _stream_handle(stream))
+        if rc != 0:
+            raise DecoderError(f"ccv_simulate_device: {_native.last_error()}")
+
+    def simulate_frames(self, seed, first_block, nblocks, channel_param, d_channel, d_info=None,
+                        stream=None, hard_demap=False):
+        """The on-device channel's frames only (ccv_simulate_device with CCV_CHANNEL_FRAMES_ONLY):
+        info bytes into d_info and the decoder input into d_channel, no decode; any plan (Viterbi,
+        stack, Fano), any code with n <= 3."""
+        flags = CHANNEL_FRAMES_ONLY | (CHANNEL_HARD_DEMAP if hard_demap else 0)
+        rc = self._lib.ccv_simulate_device(self._h, int(seed), int(first_block), int(nblocks),
+                                           float(channel_param), flags, _ptr(d_info), None, None, None,
+                                           _ptr(d_channel), _stream_handle(stream))
         if rc != 0:
             raise DecoderError(f"ccv_simulate_device: {_native.last_error()}")
 

@@ -102,7 +102,8 @@ class DeviceChannelDecoder:
     blocks of the point's Philox stream, so they go to the device in chunks of `chunk_blocks` (104
     frames for the Viterbi kernels: enough groups for every resident wave). For the stack / Fano
     decoders the on-device channel writes its output (the demapped floats or the BSC symbols) into one
-    HBM chunk buffer that the sequential decoder then reads, with its error count fused."""
+    HBM chunk buffer that the sequential decoder then reads, with its error count fused (frames only:
+    no Viterbi plan and no decode of the chunk beside the sequential one)."""
 
     def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None,
                  hard_demap=False, decoder: str = "viterbi", chunk_blocks: Optional[int] = None):
@@ -114,9 +115,11 @@ class DeviceChannelDecoder:
         if chunk_blocks is None:
             chunk_blocks = frame_blocks * max(1, (2_600_000 if decoder == "viterbi" else 200_000) // frame_blocks)
         self.chunk = chunk_blocks
-        self.plan = Plan(code, channel)            # the channel (and, for Viterbi, the decoder)
-        self.plan.reserve(self.chunk)
+        # Viterbi: one plan generates and decodes (fused); stack / Fano: the sequential plan itself
+        # generates the frames (CCV_CHANNEL_FRAMES_ONLY, no Viterbi plan, any K) and then decodes them
         self.seq = None if decoder == "viterbi" else _make_plan(code, channel, decoder)
+        self.plan = Plan(code, channel) if self.seq is None else self.seq
+        self.plan.reserve(self.chunk)
         self.channel, self.frame_blocks, self.seed = channel, frame_blocks, seed
         self.hard_demap = hard_demap
         self.d_err = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -128,7 +131,6 @@ class DeviceChannelDecoder:
             self.d_info = torch.empty((self.chunk, code.info_bytes), dtype=torch.uint8, device=self.device)
             self.d_out = torch.empty((self.chunk, code.out_bytes), dtype=torch.uint8, device=self.device)
             self.d_pm = torch.empty(self.chunk, dtype=torch.int32, device=self.device)
-            self.d_scratch_err = torch.zeros(1, dtype=torch.int64, device=self.device)
 
     def __call__(self, point: float, first_block: int, nblocks: int) -> int:
         """Bit errors of blocks first_block .. first_block + nblocks - 1 at Eb/N0 (dB) or p_ppm `point`."""
@@ -141,9 +143,8 @@ class DeviceChannelDecoder:
                 self.plan.simulate_device(self.seed, first, nb, param, d_errors=self.d_err,
                                           stream=stream, hard_demap=self.hard_demap)
                 continue
-            self.plan.simulate_device(self.seed, first, nb, param,
-                                      d_errors=self.d_scratch_err, d_info=self.d_info,
-                                      d_channel=self.d_ch, stream=stream, hard_demap=self.hard_demap)
+            self.seq.simulate_frames(self.seed, first, nb, param, self.d_ch, d_info=self.d_info,
+                                     stream=stream, hard_demap=self.hard_demap)
             self.seq.decode_device(self.d_ch, nb, self.d_out,
                                    d_path_metric=self.d_pm if self.channel == HARD else None,
                                    d_info=self.d_info, d_errors=self.d_err, stream=stream)
@@ -279,6 +280,10 @@ def main(argv=None, decode=None):
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
                     help="process-group backend (default nccl = RCCL over xGMI)")
     ap.add_argument("--out", default=None, help="also write the points as a JSON list (rank 0)")
+    ap.add_argument("--first-point-index", type=int, default=0,
+                    help="Philox stream index of the first point (point k draws stream first + k): a sweep "
+                         "split over several invocations reproduces the frames of one call when each part "
+                         "passes the index its first point had there")
     args = ap.parse_args(argv)
 
     if launch.needs_launch(args.gpus):
@@ -328,7 +333,8 @@ def main(argv=None, decode=None):
         (pt,) = ber_sweep(code, [p], channel, bits_per_point=bits_fn, frame_blocks=args.frame_blocks,
                           seed=args.seed, rank=rank, world=world, decode=decode or gpu,
                           threads=args.threads, reduce=False, hard_demap=args.hard_demap,
-                          decoder=args.decoder, point_index=k, device_decoder=dev)
+                          decoder=args.decoder, point_index=args.first_point_index + k,
+                          device_decoder=dev)
         secs[k] = time.perf_counter() - t0
         counters[k] = (pt.errors, pt.bits)
     if world > 1:
@@ -347,7 +353,8 @@ def main(argv=None, decode=None):
                "errors": errors, "bits": bits, "ber": errors / bits if bits else None,
                "ber_99.9_binomial": [lo, hi], "seconds": round(float(secs[k]), 4),
                "mbit_s": round(bits / secs[k] / 1e6, 1) if secs[k] > 0 else None,
-               "world_size": world, "device_channel": bool(args.device_channel)}
+               "world_size": world, "device_channel": bool(args.device_channel),
+               "point_index": args.first_point_index + k, "seed": args.seed}
         results.append(rec)
         if rank == 0:
             print(json.dumps(rec), flush=True)

@@ -200,7 +200,8 @@ constexpr size_t wide_slot_bytes(int main_steps) {
 }
 
 // ABLATE (timing studies, tools/k9_bench.hip; production 0): 1 decisions discarded, 2 no traceback
-// loads, 4 input with the default cache policy, 16 drain the decision stores before the traceback,
+// loads, 4 input with the default cache policy, 16 (round 3: drain the decision stores before the
+// traceback; the production default since round 4),
 // 32 packed without the position table (wrong output), 64 packed upper words padded to a dwordx4.
 // PACK: decision words per step. 0: 8, the collapsed upper bits filled in from the lower words;
 // 1: 6, the 128 lower decisions and the 43 non-collapsed upper ones dense (0.91x the time of 0);
@@ -354,9 +355,12 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
     // step m (the output of step m) at the bottom; its low K-1 bits are always the current state.
     uint64_t h = argmin_wide<S>(M);
     // The decision words come back in quarters of the block, two quarters in flight: a quarter is
-    // walked while the next one loads (the loads queue behind this wave's own stores to the same
-    // addresses, which they therefore see; AB & 16: drain the stores first, as the first cut did).
-    if constexpr ((ABLATE & 16) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // walked while the next one loads. The group's stores are drained first (vmcnt(0): L2 has
+    // acknowledged them) and the loads are agent-scope (sc1), so they miss the CU's L1, which may
+    // still hold this slot's lines from the previous group: the words read are the ones just stored,
+    // by the memory model rather than by same-address ordering (round 4; the drain measured within
+    // 1 % in round 3, profiles/r03_k9_traceback_batches.txt).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     constexpr int Q = BLEN / 4;
     static_assert(BLEN % 4 == 0, "quarters");
     uint32_t dw[2][Q][W];
@@ -372,10 +376,11 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
           asm volatile("" : "+v"(lo), "+v"(hi4), "+v"(hi2));
         } else {
           const int m = qi * Q + i;
-          lo = __builtin_amdgcn_raw_buffer_load_b128(slot, col, m * STEPB, 0);
-          if constexpr (WS == 1) hi2 = u32x2{__builtin_amdgcn_raw_buffer_load_b32(slot, colh, m * STEPB + 1024, 0), 0u};
-          else if constexpr (WS == 2) hi2 = __builtin_amdgcn_raw_buffer_load_b64(slot, colh, m * STEPB + 1024, 0);
-          else hi4 = __builtin_amdgcn_raw_buffer_load_b128(slot, colh, m * STEPB + 1024, 0);
+          constexpr int kSc1 = 16;   // cache policy: agent scope (sc1)
+          lo = __builtin_amdgcn_raw_buffer_load_b128(slot, col, m * STEPB, kSc1);
+          if constexpr (WS == 1) hi2 = u32x2{__builtin_amdgcn_raw_buffer_load_b32(slot, colh, m * STEPB + 1024, kSc1), 0u};
+          else if constexpr (WS == 2) hi2 = __builtin_amdgcn_raw_buffer_load_b64(slot, colh, m * STEPB + 1024, kSc1);
+          else hi4 = __builtin_amdgcn_raw_buffer_load_b128(slot, colh, m * STEPB + 1024, kSc1);
           if constexpr (WS == 4 && WH == 2) hi2 = u32x2{hi4.x, hi4.y};
         }
         dw[qi & 1][i][0] = lo.x; dw[qi & 1][i][1] = lo.y; dw[qi & 1][i][2] = lo.z; dw[qi & 1][i][3] = lo.w;

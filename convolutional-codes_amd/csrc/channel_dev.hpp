@@ -151,12 +151,45 @@ struct Encoder {
 
 // Per-lane source of one block's decoder input, in decoder order. HARD: BM = Hamming distances of
 // the received symbol; soft: BM = demapped squared distances.
-template <CodeSpec C, bool HARD>
+// Encoder of a code known only at run time (ccv_simulate_device CCV_CHANNEL_FRAMES_ONLY: any plan, K <=
+// 64): the same register window and shift-register arithmetic as Encoder<C>, with a 64-bit state.
+template <int NP>
+struct EncoderRT {
+  uint32_t w[8];
+  uint64_t state;
+  int t;
+  int K, gen;
+  uint64_t poly[NP];
+  __device__ __forceinline__ uint32_t symbol_and_advance(int blen) {
+    const uint64_t i = t < blen ? (w[0] >> 31) : 0u;
+    const uint64_t sr = (K < 64 ? state << (64 - K) : state) | (i << 63);
+    uint32_t e = 0;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const uint64_t v = sr & poly[k];
+      uint32_t p = (uint32_t)__popcll(v) & 1u;
+      if (gen == GEN_REF_X86) p &= ((uint32_t)__popcll(v & 0x1010101010101010ull) & 1u) ^ 1u;
+      e = (e << 1) | p;
+    }
+    state = (state >> 1) | (i << (K - 2));
+    ++t;
+    if ((t & 31) == 0) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) w[k] = w[k + 1];
+      w[7] = 0;
+    } else {
+      w[0] <<= 1;
+    }
+    return e;
+  }
+};
+
+template <CodeSpec C, bool HARD, class Enc = Encoder<C>>
 struct ChannelSource {
   static constexpr int NS = 1 << C.n;
   using MT = typename std::conditional<HARD, uint32_t, float>::type;
   Philox rng;
-  Encoder<C> enc;
+  Enc enc;
   int T, blen;
   float scaling;
   int32_t p_ppm;
@@ -467,6 +500,34 @@ __global__ __launch_bounds__(kRegThreads) void channel_frames(ChanArgs a) {
       if (sub < n && b0 + r < nb) frame[(size_t)(b0 + r) * T + c0 + sub] = stage[sub][r];
     }
     __syncthreads();
+  }
+}
+
+// Frames only, any code (CCV_CHANNEL_FRAMES_ONLY): one lane per block writes the info bytes and the
+// decoder input of its block (float [T][2^n] or uint8 [T]) in the same draw order, with no decode --
+// the producer of the sequential decoders' device sweeps (K = 15, WSPR K = 32). Rows are written by
+// the source's per-step export (a lane's own row; these decoders take far longer than the channel).
+struct CodeRT {
+  int K, gen;
+  uint64_t poly[3];
+};
+template <int NP, bool HARD>
+__global__ __launch_bounds__(kRegThreads) void channel_frames_rt(ChanArgs a, CodeRT code) {
+  constexpr CodeSpec C{NP, 3, {0, 0, 0, 0, 0, 0, 0, 0}, GEN_REF_X86};   // n only: the encoder is RT
+  using Src = ChannelSource<C, HARD, EncoderRT<NP>>;
+  using MT = typename Src::MT;
+  const int b = blockIdx.x * kRegThreads + threadIdx.x;
+  if (b >= a.r.nblocks) return;
+  Src src;
+  src.enc.K = code.K;
+  src.enc.gen = code.gen;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) src.enc.poly[k] = code.poly[k];
+  src.init(a, b, true);
+#pragma unroll 1
+  for (int t = 0; t < a.r.T; ++t) {
+    MT BM[Src::NS];
+    src.next(BM);
   }
 }
 

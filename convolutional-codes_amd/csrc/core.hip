@@ -166,7 +166,8 @@ ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
   return ccv::soft_regdec_launchers()[p.reg_index];
 }
 
-// The one-lane-per-block persistent K = 9 kernel (acs_wide.hpp; the x86-idiom code, soft), or
+// The persistent K = 9 soft kernel with a per-wave decision slot (acs_wide.hpp one lane per block for
+// the x86-idiom code, acs_multi.hpp viterbi_multi_slot four lanes per block for true parity), or
 // nullptr: codebook block length, block-major input, decisions not exported.
 ccv::RegLaunchFn wide_kernel(const ccv_plan& p, bool export_decisions) {
   if (p.no_persistent || p.global_decisions || export_decisions || p.step_major ||
@@ -267,9 +268,16 @@ hipError_t launch_service_t(const ccv::GenericArgs& a, const ccv_plan& p, ccv::S
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  // idle 20 ms of the 100 MHz real-time counter, at most 2,000,000 polls (~2-4 s)
+  // idle CCV_SERVICE_IDLE_MS (default 20 ms) of the 100 MHz real-time counter, at most 2,000,000 polls
+  // (~2-4 s): while it idles the kernel keeps one workgroup resident and a device-wide synchronise
+  // in the process waits for it (include/ccv.h)
+  uint64_t idle_ticks = 2000000;
+  if (const char* env = std::getenv("CCV_SERVICE_IDLE_MS")) {
+    const long ms = std::atol(env);
+    idle_ticks = ms <= 0 ? 1 : (uint64_t)(ms > 2000 ? 2000 : ms) * 100000u;
+  }
   hipLaunchKernelGGL((ccv::viterbi_service<SPT, HARD, LATN>), dim3(1), dim3(LATN ? 64 : p.generic_threads), lds, s,
-                     a, mb, served, (uint64_t)2000000, (uint32_t)2000000);
+                     a, mb, served, idle_ticks, (uint32_t)2000000);
   return hipGetLastError();
 }
 
@@ -458,7 +466,7 @@ const char* ccv_plan_kernel_variant(const ccv_plan* p) {
   if (p->stack) return "stack";
   if (p->fano) return "fano";
   if (!register_path(*p)) return "generic";
-  if (wide_kernel(*p, false)) return "persistent-wide";
+  if (wide_kernel(*p, false)) return p->d.gen_mode == CCV_GEN_REF_X86 ? "persistent-wide" : "persistent-slot";
   if (persist_kernel(*p, false)) return "persistent";
   if (p->multi_index >= 0) return regdec_kernel(*p, false) ? "multilane-regdec" : "multilane";
   return regdec_kernel(*p, false) ? "register-regdec" : "register";
@@ -481,7 +489,7 @@ int persistent_grid(ccv::RegLaunchFn persist, bool fresh) {
 int grow_wide_scratch(ccv_plan& p, ccv::RegLaunchFn wide, hipStream_t stream) {
   const int waves = persistent_grid(wide, false);
   if (waves <= 0) return waves < 0 ? -1 : fail("no resident waves for the K = 9 kernel");
-  return p.dec.grow((size_t)waves * ccv::multi_wide_slot_bytes(), stream);
+  return p.dec.grow((size_t)waves * ccv::multi_wide_slot_bytes(p.multi_index), stream);
 }
 }  // namespace
 
@@ -537,10 +545,12 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     a.info = d_info;
     a.err = d_info ? d_errors : nullptr;
     if (const ccv::RegLaunchFn wide = wide_kernel(*p, d_decisions != nullptr)) {
-      // one lane per block, groups of 64 blocks, decisions in a per-wave scratch slot (acs_wide.hpp)
+      // decisions in a per-wave scratch slot, groups of 64 (one lane per block, acs_wide.hpp) or 16
+      // (four lanes per block, acs_multi.hpp viterbi_multi_slot) blocks
       if (grow_wide_scratch(*p, wide, stream)) return -1;
       a.dec = p->dec.ptr;
-      HIP_TRY(wide(a, (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads), stream));
+      const size_t gb = (size_t)ccv::multi_wide_group_blocks(p->multi_index);
+      HIP_TRY(wide(a, (int)((nblocks + gb - 1) / gb), stream));
       return 0;
     }
     if (const ccv::RegLaunchFn persist = persist_kernel(*p, d_decisions != nullptr)) {
@@ -827,13 +837,51 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
   return 0;
 }
 
+// CCV_CHANNEL_FRAMES_ONLY: the channel's frames (info bytes, decoder input) for any plan's code, no
+// decode (channel_dev.hpp channel_frames_rt) -- the producer of the stack / Fano device sweeps.
+static int simulate_frames_only(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t nblocks,
+                                double channel_param, unsigned channel_flags, uint8_t* d_info,
+                                void* d_channel, void* stream_v) {
+  const bool hard = p->d.channel == CCV_HARD;
+  if (!d_channel) return fail("CCV_CHANNEL_FRAMES_ONLY needs d_channel");
+  if (p->d.n > 3) return fail("frames-only channel: n = %d (n <= 3)", p->d.n);
+  if (hard && !(channel_param >= 0.0 && channel_param <= 1000000.0))
+    return fail("BSC p_ppm must be in [0, 1e6]");
+  if (!hard && !(channel_param >= 0.0 && channel_param < 268435456.0))
+    return fail("AWGN noise scaling must be in [0, 2^28)");
+  if (hard && (channel_flags & CCV_CHANNEL_HARD_DEMAP)) return fail("the hard demapper belongs to the AWGN channel");
+  if (nblocks == 0) return 0;
+  if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
+  if (!d_info) {
+    if (p->sim_info.grow(nblocks * (size_t)p->d.info_bytes, stream)) return -1;
+    d_info = static_cast<uint8_t*>(p->sim_info.ptr);
+  }
+  ccv::ChanArgs a{};
+  a.r.T = p->d.steps;
+  a.r.nblocks = (int)nblocks;
+  a.r.blen = p->d.blen;
+  a.seed = seed;
+  a.first_block = first_block;
+  a.scaling = (float)channel_param;
+  a.p_ppm = hard ? (int32_t)channel_param : 0;
+  a.hard_demap = (channel_flags & CCV_CHANNEL_HARD_DEMAP) != 0;
+  a.info_out = d_info;
+  a.ch_out = d_channel;
+  HIP_TRY(ccv::launch_channel_frames_any(a, p->d.n, p->d.K, p->polys, p->d.gen_mode, hard, stream));
+  return 0;
+}
+
 int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,
                         int32_t* d_path_metric, unsigned long long* d_errors, void* d_channel,
                         void* stream_v) {
   if (!p) return fail("null plan");
+  if (channel_flags & CCV_CHANNEL_FRAMES_ONLY)
+    return simulate_frames_only(p, seed, first_block, nblocks, channel_param, channel_flags, d_info,
+                                d_channel, stream_v);
   if (p->stack || p->fano)
-    return fail("the on-device channel is implemented for the Viterbi kernels");
+    return fail("a sequential-decoder plan takes the on-device channel with CCV_CHANNEL_FRAMES_ONLY");
   if (!register_path(*p))
     return fail("the on-device channel needs a register-trellis code (K <= 9 with a specialised kernel)");
   if (p->d.channel == CCV_SOFT && p->d.n > 3)
@@ -996,7 +1044,13 @@ static int decode_host_service(ccv_plan* p, const void* in, size_t nblocks, uint
       if (launch(seq - 1)) return -1;
     }
     if ((spins & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      // end the kernel before giving up: a service left polling could answer the NEXT call's request
+      // (and a relaunched one decode it again). It exits on `stop` or after its bounded poll count.
+      __atomic_store_n(&mb->stop, 1u, __ATOMIC_RELEASE);
+      const hipError_t e = hipStreamSynchronize(p->svc_stream);
+      __atomic_store_n(&mb->stop, 0u, __ATOMIC_RELEASE);
       p->svc_running = false;
+      if (e != hipSuccess) return fail("streaming service: %s", hipGetErrorString(e));
       return fail("streaming service did not answer within 10 s");
     }
     __builtin_ia32_pause();

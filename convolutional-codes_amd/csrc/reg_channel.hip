@@ -65,6 +65,22 @@ constexpr auto kFrames = make_frames(std::make_index_sequence<kNumMultiCodes>{})
 
 const ChanLaunchFn* channel_frames_launchers() { return kFrames.data(); }
 
+hipError_t launch_channel_frames_any(const ChanArgs& a, int n, int K, const uint64_t* polys, int gen,
+                                     bool hard, hipStream_t stream) {
+  CodeRT code{K, gen, {polys[0], n > 1 ? polys[1] : 0, n > 2 ? polys[2] : 0}};
+  const dim3 grid((unsigned)((a.r.nblocks + kRegThreads - 1) / kRegThreads)), block(kRegThreads);
+  switch ((hard ? 4 : 0) + n) {
+    case 1: hipLaunchKernelGGL((channel_frames_rt<1, false>), grid, block, 0, stream, a, code); break;
+    case 2: hipLaunchKernelGGL((channel_frames_rt<2, false>), grid, block, 0, stream, a, code); break;
+    case 3: hipLaunchKernelGGL((channel_frames_rt<3, false>), grid, block, 0, stream, a, code); break;
+    case 5: hipLaunchKernelGGL((channel_frames_rt<1, true>), grid, block, 0, stream, a, code); break;
+    case 6: hipLaunchKernelGGL((channel_frames_rt<2, true>), grid, block, 0, stream, a, code); break;
+    case 7: hipLaunchKernelGGL((channel_frames_rt<3, true>), grid, block, 0, stream, a, code); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 const ChanLaunchFn* channel_launchers(bool multi, bool hard) {
   if (multi) return hard ? kMultiHard.data() : kMultiSoft.data();
   return hard ? kRegHard.data() : kRegSoft.data();

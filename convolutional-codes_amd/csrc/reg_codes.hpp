@@ -65,13 +65,16 @@ int multi_regdec_max_steps(int K);
 // groups of 64 / 2^(K-7) blocks), nullptr where a code has none (K = 9, r = 1/2 only); valid for
 // blen == kPersistBlen, block-major input, no decision export (reg_multi.hip)
 const RegLaunchFn* multi_persist_launchers();
-// [kNumMultiCodes] one-lane-per-block persistent soft kernel (acs_wide.hpp viterbi_wide_persist;
-// int argument = groups of 64 blocks), nullptr where a code has none (the K = 9 x86-idiom code:
-// 156 distinct metrics fit one lane's VGPRs; the true-parity trellis has 256). RegArgs::dec = one
-// scratch slot of multi_wide_slot_bytes() per resident wave of the grid. Valid for blen ==
-// kPersistBlen, block-major input, no decision export (reg_multi.hip)
+// [kNumMultiCodes] persistent soft kernels whose decisions go through a per-wave scratch slot,
+// nullptr where a code has none: the K = 9 x86-idiom code runs one lane per block (acs_wide.hpp
+// viterbi_wide_persist: 156 distinct metrics fit one lane's VGPRs), the true-parity K = 9 code four
+// lanes per block with its main periods as a loop (acs_multi.hpp viterbi_multi_slot). int argument =
+// groups of multi_wide_group_blocks(index) blocks; RegArgs::dec = one scratch slot of
+// multi_wide_slot_bytes(index) per resident wave of the grid. Valid for blen == kPersistBlen,
+// block-major input, no decision export (reg_multi.hip)
 const RegLaunchFn* multi_wide_launchers();
-size_t multi_wide_slot_bytes();
+size_t multi_wide_slot_bytes(int index);
+int multi_wide_group_blocks(int index);
 
 struct ChanArgs;
 using ChanLaunchFn = hipError_t (*)(const ChanArgs&, int grid, hipStream_t stream);
@@ -80,5 +83,9 @@ const ChanLaunchFn* channel_launchers(bool multi, bool hard);
 // [kNumMultiCodes] frames-only soft channel (channel_dev.hpp channel_frames): info bytes and the
 // decoder input [nb][T][4] written to ChanArgs::info_out / ch_out, grid = one lane per block
 const ChanLaunchFn* channel_frames_launchers();
+// frames only for any code with n <= 3 and K <= 64 (channel_dev.hpp channel_frames_rt; one lane per
+// block, ChanArgs::info_out and ch_out required), reg_channel.hip
+hipError_t launch_channel_frames_any(const ChanArgs& a, int n, int K, const uint64_t* polys, int gen,
+                                     bool hard, hipStream_t stream);
 
 }  // namespace ccv

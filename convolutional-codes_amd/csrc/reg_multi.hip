@@ -50,27 +50,56 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence
   return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2) ? &launch_persist<I> : nullptr)...};
 }
 
+// Codes with a slot kernel (decisions through a per-wave scratch slot): K = 9 r = 1/2
+template <size_t I>
+constexpr bool has_slot_kernel() {
+  return kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2;
+}
+
 template <size_t I>
 hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
-  // one lane per block, one decision per value-numbering class (156 of 256 states, twins.hpp)
-  // through a per-wave scratch slot: ~0.57x the time of the four-lane kernel below at 32 frames,
-  // bit-identical (tools/k9_bench.hip, profiles/r03_k9_wide*.txt)
-  if constexpr (kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2 && kMultiCodes[I].gen == GEN_REF_X86)
+  if constexpr (has_slot_kernel<I>() && kMultiCodes[I].gen == GEN_REF_X86)
+    // one lane per block, one decision per value-numbering class (156 of 256 states, twins.hpp)
+    // through a per-wave scratch slot: ~0.57x the time of the four-lane kernel at 32 frames,
+    // bit-identical (tools/k9_bench.hip, profiles/r03_k9_wide*.txt)
     return launch_persistent(viterbi_wide_persist<kMultiCodes[I], kPersistBlen, 0, 2>, a, ngroups, stream);
+  else if constexpr (has_slot_kernel<I>())
+    // true parity (256 distinct metrics): four lanes per block, the main periods as a loop with the
+    // decisions through a per-wave slot, so the code fits the instruction cache (acs_multi.hpp
+    // viterbi_multi_slot)
+    return launch_persistent(viterbi_multi_slot<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
   else
     return hipErrorInvalidValue;
 }
 
 template <size_t... I>
 constexpr std::array<RegLaunchFn, sizeof...(I)> make_wide(std::index_sequence<I...>) {
-  return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2 && kMultiCodes[I].gen == GEN_REF_X86)
-               ? &launch_wide<I>
-               : nullptr)...};
+  return {(has_slot_kernel<I>() ? &launch_wide<I> : nullptr)...};
+}
+
+template <size_t I>
+constexpr size_t slot_bytes() {
+  if constexpr (!has_slot_kernel<I>()) return 0;
+  else if constexpr (kMultiCodes[I].gen == GEN_REF_X86) return wide_slot_bytes<kMultiCodes[I], 2>(kPersistBlen);
+  else return multi_slot_bytes<kMultiCodes[I], kPersistBlen>();
+}
+
+template <size_t... I>
+constexpr std::array<size_t, sizeof...(I)> make_slot_bytes(std::index_sequence<I...>) {
+  return {slot_bytes<I>()...};
+}
+
+template <size_t... I>
+constexpr std::array<int, sizeof...(I)> make_group_blocks(std::index_sequence<I...>) {
+  return {(!has_slot_kernel<I>() ? 0 : kMultiCodes[I].gen == GEN_REF_X86 ? kRegThreads
+                                                                         : kRegThreads / Multi<kMultiCodes[I]>::L)...};
 }
 
 constexpr auto kSoft = make<false>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kSoftPersist = make_persist(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kSoftWide = make_wide(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kSlotBytes = make_slot_bytes(std::make_index_sequence<kNumMultiCodes>{});
+constexpr auto kSlotGroupBlocks = make_group_blocks(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kHard = make<true>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kSoftRegDec = make_regdec<false>(std::make_index_sequence<kNumMultiCodes>{});
 constexpr auto kHardRegDec = make_regdec<true>(std::make_index_sequence<kNumMultiCodes>{});
@@ -83,7 +112,9 @@ const RegLaunchFn* multi_persist_launchers() { return kSoftPersist.data(); }
 
 const RegLaunchFn* multi_wide_launchers() { return kSoftWide.data(); }
 
-size_t multi_wide_slot_bytes() { return wide_slot_bytes<kMultiCodes[2], 2>(kPersistBlen); }
+size_t multi_wide_slot_bytes(int index) { return kSlotBytes[(size_t)index]; }
+
+int multi_wide_group_blocks(int index) { return kSlotGroupBlocks[(size_t)index]; }
 
 const RegLaunchFn* multi_regdec_launchers(bool hard) {
   return hard ? kHardRegDec.data() : kSoftRegDec.data();

@@ -276,10 +276,13 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode(StackArgs a) {
 //     as a second u32 min reduction over per-lane candidates;
 //   * all bookkeeping (frontier t, stack size, status) is row-uniform VALU state, so the four
 //     searches share one instruction stream and the scalar unit only runs the loop;
-//   * metrics stay in VGPRs (4 slots per lane, for the scans); the rest of an entry -- next index
+//   * the 64 path metrics live in LDS next to the records (lane l reads its kRowSlots entries as one
+//     ds_read_b128 at the top of each iteration, for the scans); the rest of an entry -- next index
 //     and expected symbols packed, 32-bit encoder state, 64 path bits -- is one 16-byte LDS record
 //     per entry, so the current path's record is one broadcast ds_read_b128 and an update one
 //     ds_write_b128 by the row's lane 0 (current path) and lane 1 (duplicate);
+//   * the most- and least-probable scans read the same metrics, so they run as ONE interleaved pair
+//     of row reductions (values, then indices): each fills the other's DPP hazard slots (round 4);
 //   * rows are persistent: a row that finishes its block writes the output and takes the next
 //     block from a global counter, so a long search holds up only its own row.
 // Same arithmetic, tie rules and streaming quirks as stack_decode (the previous block's symbols
@@ -310,6 +313,32 @@ CCV_ROW_FN(row_min_u32, uint32_t, "v_min_u32")
 #undef CCV_ROW_REDUCE8
 #undef CCV_ROW_REDUCE
 #undef CCV_ROW_STEP
+
+// Two independent row reductions in ONE asm block, their DPP steps interleaved: a DPP read needs two
+// wait states after the VALU write of its source, and the other chain's step fills one of them, so
+// each step pair costs one s_nop 0 instead of the two s_nop 1 of two separate reductions (the
+// most- and least-probable scans of a search iteration read the same metrics and are independent).
+#define CCV_ROW_STEP2(opa, opb, ctrl)                                                          \
+  opa "_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf\n" opb "_dpp %1, %1, %1 " ctrl      \
+      " row_mask:0xf bank_mask:0xf\n"
+#define CCV_ROW_REDUCE2_8(opa, opb)                                                            \
+  "s_nop 1\n" CCV_ROW_STEP2(opa, opb, "quad_perm:[1,0,3,2]") "s_nop 0\n"                       \
+      CCV_ROW_STEP2(opa, opb, "quad_perm:[2,3,0,1]") "s_nop 0\n"                               \
+      CCV_ROW_STEP2(opa, opb, "row_half_mirror")
+#define CCV_ROW_REDUCE2(opa, opb) CCV_ROW_REDUCE2_8(opa, opb) "s_nop 0\n" CCV_ROW_STEP2(opa, opb, "row_mirror")
+#define CCV_ROW_FN2(name, TA, TB, opa, opb)                                                    \
+  template <int RL>                                                                            \
+  __device__ __forceinline__ void name(TA& a, TB& b) {                                         \
+    if constexpr (RL == 16) asm volatile(CCV_ROW_REDUCE2(opa, opb) : "+v"(a), "+v"(b));        \
+    else asm volatile(CCV_ROW_REDUCE2_8(opa, opb) : "+v"(a), "+v"(b));                         \
+  }
+CCV_ROW_FN2(row_max_min, float, float, "v_max_f32", "v_min_f32")
+CCV_ROW_FN2(row_max_min, int32_t, int32_t, "v_max_i32", "v_min_i32")
+CCV_ROW_FN2(row_min_min_u32, uint32_t, uint32_t, "v_min_u32", "v_min_u32")
+#undef CCV_ROW_FN2
+#undef CCV_ROW_REDUCE2_8
+#undef CCV_ROW_REDUCE2
+#undef CCV_ROW_STEP2
 
 // max / min without the canonicalising v_max x,x hipcc wraps around fmaxf (IEEE max/min skip NaN,
 // as the reference's strict compares do)
@@ -422,27 +451,42 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       MT met[kRowSlots];
 #pragma unroll
       for (int k = 0; k < kRowSlots; ++k) met[k] = metl[l * kRowSlots + k];
-      MT mx;
-      uint32_t cur;
+      // ... and duplicate_path's least probable entry (:227-241, strict < from +inf, first index
+      // wins) from the same metrics: both scans run as one interleaved pair of row reductions
+      MT mx, mn;
+      uint32_t cur, c2;
       bool ok;
       if constexpr (KEY) {
-        int32_t kx = INT32_MIN;
+        int32_t kx = INT32_MIN, kn = INT32_MAX;
 #pragma unroll
-        for (int k = 0; k < kRowSlots; ++k)
+        for (int k = 0; k < kRowSlots; ++k) {
           kx = vmax2(kx, (int32_t)((uint32_t)met[k] * 64u) + (63 - (l * kRowSlots + k)));
-        kx = row_max<RL>(kx);
+          kn = vmin2(kn, (int32_t)((uint32_t)met[k] * 64u) + (l * kRowSlots + k));
+        }
+        row_max_min<RL>(kx, kn);
         mx = (MT)(kx >> 6);
         cur = 63u - ((uint32_t)kx & 63u);
         ok = kx > -(1 << 30);
+        mn = (MT)(kn >> 6);
+        c2 = (uint32_t)kn & 63u;
       } else {
         mx = met[0];
+        mn = met[0];
 #pragma unroll
-        for (int k = 1; k < kRowSlots; ++k) mx = vmax2(mx, met[k]);
-        mx = row_max<RL>(mx);
+        for (int k = 1; k < kRowSlots; ++k) {
+          mx = vmax2(mx, met[k]);
+          mn = vmin2(mn, met[k]);
+        }
+        row_max_min<RL>(mx, mn);
         uint32_t cand = kStackDepth;
+        c2 = kStackDepth;
 #pragma unroll
-        for (int k = kRowSlots - 1; k >= 0; --k) cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
-        cur = row_min_u32<RL>(cand);
+        for (int k = kRowSlots - 1; k >= 0; --k) {
+          cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
+          c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
+        }
+        row_min_min_u32<RL>(cand, c2);
+        cur = cand;
         ok = mx > lo_sent;
       }
       // the common path is branch-free: every quantity is computed, the outcome selected
@@ -485,28 +529,8 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
         tm0 = (float)(1.0 + (double)(a.weight * r0));   // AWGN-channel/stack-decoder.c:274
         tm1 = (float)(1.0 + (double)(a.weight * r1));
       }
-      // duplicate_path (:227-241): a free entry, or the least probable one (strict < from +inf)
+      // duplicate_path (:227-241): a free entry, or the least probable one (mn / c2 above)
       const bool full = size == kStackDepth;
-      MT mn;
-      uint32_t c2;
-      if constexpr (KEY) {
-        int32_t kn = INT32_MAX;
-#pragma unroll
-        for (int k = 0; k < kRowSlots; ++k)
-          kn = vmin2(kn, (int32_t)((uint32_t)met[k] * 64u) + (l * kRowSlots + k));
-        kn = row_min<RL>(kn);
-        mn = (MT)(kn >> 6);
-        c2 = (uint32_t)kn & 63u;
-      } else {
-        mn = met[0];
-#pragma unroll
-        for (int k = 1; k < kRowSlots; ++k) mn = vmin2(mn, met[k]);
-        mn = row_min<RL>(mn);
-        c2 = kStackDepth;
-#pragma unroll
-        for (int k = kRowSlots - 1; k >= 0; --k) c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
-        c2 = row_min_u32<RL>(c2);
-      }
       const bool dbad = ext && full && !(mn < hi_sent);
       bad = bad || dbad;
       ext = ext && !dbad;

@@ -127,6 +127,10 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
  * run as two kernels instead: the frames into d_channel (or plan scratch), then the persistent decode
  * (same draws, same results; CCV_CHANNEL_FUSED=1 forces the fused kernel). */
 #define CCV_CHANNEL_HARD_DEMAP 1u   /* AWGN: common/hard-demapper.c instead of common/demapper.c */
+/* Frames only, no decode: info bytes into d_info (or plan scratch) and the decoder input into d_channel
+ * (required), same draws as above, for ANY plan -- Viterbi, stack or Fano, n <= 3, K <= 64. d_out,
+ * d_path_metric and d_errors are ignored. The device sweeps of the sequential decoders use it. */
+#define CCV_CHANNEL_FRAMES_ONLY 2u
 int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,
                         int32_t* d_path_metric, unsigned long long* d_errors, void* d_channel,
@@ -169,7 +173,11 @@ int ccv_fano_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uin
 int ccv_stack_decode_host(ccv_plan* plan, const void* in, size_t nblocks, const void* prev,
                           uint8_t* out, int32_t* path_metric, int32_t* status);
 
-/* Synchronous convenience: host buffers in and out (staged through plan-owned device buffers). */
+/* Synchronous convenience: host buffers in and out (staged through plan-owned device buffers).
+ * Batches of <= 4 blocks (the streaming decoder_input path) go to a resident service kernel of the
+ * plan that polls a host mailbox and stays on the GPU for CCV_SERVICE_IDLE_MS (default 20 ms) after
+ * the last request, holding one workgroup: a device-wide synchronise in the process waits for it
+ * meanwhile. CCV_HOST_LATENCY=1 launches one kernel per call instead; ccv_plan_destroy stops it. */
 int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out,
                     int32_t* path_metric);
 

@@ -92,7 +92,8 @@ def test_register_kernel_selected_for_benchmark_codes():
     # K = 8, 9 (multilane kernel): register-resident up to T = 48 (K9) / 49 (K8), soft and hard
     for c in (K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
         # the K = 9 x86-idiom soft code runs one lane per block with a per-wave decision slot
-        soft = "slot" if c is K9 else "registers"
+        # (the true-parity K = 9 code four lanes per block with a slot too, viterbi_multi_slot)
+        soft = "slot" if c.K == 9 else "registers"
         assert Plan(c, SOFT).decisions == soft and Plan(c, HARD).decisions == "registers"
         assert Plan(c, SOFT, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
         assert Plan(c, SOFT, FLAG_NO_PERSISTENT).decisions == "registers"
@@ -166,11 +167,11 @@ def test_reference_api_callback_takes_ownership(case):
     taken, copied, pms = [], [], []
     count = [0]
 
-    def take(data, length, *pm):
+    def take(data, length, *rest):   # rest: (userdata,) soft / (path_metric, userdata) hard
         assert length == c.blen
         count[0] += 1
-        if pm:
-            pms.append(int(pm[0]))
+        if not soft:
+            pms.append(int(rest[0]))
         if count[0] % 2 == 1:
             taken.append((count[0] - 1, ctypes.cast(data, ctypes.c_void_p).value))
             return 0
@@ -423,27 +424,32 @@ def test_multilane_shapes(K, nb, blen):
         assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
 
 
-@pytest.mark.parametrize("nb", [1, 63, 64, 65, 3 * 64 + 5, 150000])
-def test_k9_wide_kernel(torch_cuda, nb):
-    """K = 9 x86-idiom soft at blen 40 runs the one-lane-per-block kernel (acs_wide.hpp): ragged
-    batches and more 64-block groups than resident waves (150,000 blocks: each wave decodes several
-    groups through its one decision slot) decode exactly as the four-lane kernel (FLAG_NO_PERSISTENT)
-    and, on a sample, the oracle; the fused error count equals the host count."""
+@pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["idiom", "true"])
+@pytest.mark.parametrize("nb", [1, 15, 16, 17, 63, 64, 65, 3 * 64 + 5, 150000])
+def test_k9_wide_kernel(torch_cuda, nb, gen):
+    """K = 9 soft at blen 40 runs a persistent kernel whose decisions go through a per-wave scratch
+    slot: one lane per block for the x86-idiom code (acs_wide.hpp), four lanes per block with the main
+    periods as a loop for the true-parity code (acs_multi.hpp viterbi_multi_slot). Ragged batches and
+    more groups than resident waves (150,000 blocks: each wave decodes several groups through its one
+    slot) decode exactly as the non-persistent four-lane kernel (FLAG_NO_PERSISTENT) and, on a
+    sample, the oracle; the fused error count equals the host count."""
     torch = torch_cuda
-    plan = Plan(K9, SOFT)
-    assert plan.variant == "persistent-wide" and plan.decisions == "slot"
-    info, rx = ch.awgn_blocks(K9, nb, ch.noise_scaling(3.0), 4242 + nb)
-    d_out = torch.empty((nb, K9.out_bytes), dtype=torch.uint8, device="cuda")
+    c = K9.with_(gen_mode=gen)
+    plan = Plan(c, SOFT)
+    assert plan.variant == ("persistent-wide" if gen == GEN_REF_X86 else "persistent-slot")
+    assert plan.decisions == "slot"
+    info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 4242 + nb)
+    d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
     plan.decode_device(_device(torch, rx), nb, d_out, d_info=_device(torch, info), d_errors=d_err)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy()
-    assert int(d_err.item()) == ch.count_bit_errors(K9, info, out)
-    four_lane = Plan(K9, SOFT, FLAG_NO_PERSISTENT)
+    assert int(d_err.item()) == ch.count_bit_errors(c, info, out)
+    four_lane = Plan(c, SOFT, FLAG_NO_PERSISTENT)
     assert four_lane.variant.startswith("multilane")
     assert np.array_equal(out, four_lane.decode_host(rx))
     sample = np.unique(np.linspace(0, nb - 1, min(nb, 300)).astype(np.int64))
-    assert np.array_equal(out[sample], O.viterbi_soft(_ocode(K9), rx[sample]))
+    assert np.array_equal(out[sample], O.viterbi_soft(_ocode(c), rx[sample]))
 
 
 def test_multilane_error_count_and_no_decision_export(torch_cuda):

@@ -138,6 +138,28 @@ def test_sweep_cli_gloo_world2_matches_one_process(tmp_path, monkeypatch, capsys
         assert lo <= r["ber"] <= hi
 
 
+def test_sweep_cli_split_with_first_point_index_matches_one_call(tmp_path, monkeypatch):
+    """Point k of --points draws Philox stream --first-point-index + k: a sweep split over two
+    invocations (the second passing the index its first point had in the whole sweep) gives the same
+    counts as one call, and each record names its stream."""
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    from ccviterbi import sim
+    base = [a for a in SWEEP_ARGS]
+    i = base.index("--points")
+    whole = base[:i] + ["--points", "1,3,5"] + base[i + 2:]
+    part1 = base[:i] + ["--points", "1"] + base[i + 2:]
+    part2 = base[:i] + ["--points", "3,5", "--first-point-index", "1"] + base[i + 2:]
+    assert sim.main(whole + ["--out", str(tmp_path / "w.json")], decode=_oracle_decode()) == 0
+    assert sim.main(part1 + ["--out", str(tmp_path / "a.json")], decode=_oracle_decode()) == 0
+    assert sim.main(part2 + ["--out", str(tmp_path / "b.json")], decode=_oracle_decode()) == 0
+    w = json.load(open(tmp_path / "w.json"))
+    ab = json.load(open(tmp_path / "a.json")) + json.load(open(tmp_path / "b.json"))
+    assert [(r["errors"], r["bits"], r["point_index"]) for r in w] == \
+        [(r["errors"], r["bits"], r["point_index"]) for r in ab]
+    assert [r["point_index"] for r in w] == [0, 1, 2]
+
+
 def test_ber_interval():
     from ccviterbi.sim import ber_interval
     lo, hi = ber_interval(100, 10 ** 6)
