@@ -196,11 +196,15 @@ __device__ __forceinline__ void multi_growth_step_impl(MT (&M)[64], const MT (&B
   (multi_growth<C, P, 63 - (int)I, SAT, MT, X>(M, BM, qb0, qb1), ...);
 }
 
-template <CodeSpec C, int P, bool SAT, typename MT, class X = Multi<C>, size_t... I>
+template <CodeSpec C, int P, bool SAT, typename MT, class X = Multi<C>, int GRP = 0, size_t... I>
 __device__ __forceinline__ uint64_t multi_step_impl(MT (&M)[64], const MT (&BM)[1 << C.n], bool qb0,
                                                     bool qb1, std::index_sequence<I...>) {
   uint32_t lo = 0, hi = 0;
-  (multi_acs<C, P, 63 - (int)I, SAT, MT, X>(M, BM, qb0, qb1, lo, hi), ...);   // descending registers
+  // descending registers; GRP > 0: a scheduling barrier after every GRP registers (bounds the live
+  // temporaries where the register budget is tight)
+  ((multi_acs<C, P, 63 - (int)I, SAT, MT, X>(M, BM, qb0, qb1, lo, hi),
+    (GRP && (I + 1) % GRP == 0 ? __builtin_amdgcn_sched_barrier(0) : (void)0)),
+   ...);
   return ((uint64_t)hi << 32) | lo;
 }
 
@@ -783,6 +787,9 @@ constexpr size_t multi_slot_bytes() {
   return (size_t)(BLEN + C.K - 1 - (C.K - 1)) * kRegThreads * 8;   // main steps x 64 lanes x 8 B
 }
 
+#ifndef CCV_SLOT_GROUP
+#define CCV_SLOT_GROUP 0
+#endif
 template <CodeSpec C, int BLEN, int WAVES = 3, int LB0 = 0, int LB1 = 3>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(WAVES)))
 void viterbi_multi_slot(RegArgs a, int ngroups) {
@@ -807,16 +814,20 @@ void viterbi_multi_slot(RegArgs a, int ngroups) {
   const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
   const int nb = a.nblocks;
   const int stride_groups = gridDim.x;
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[BUF];
+  // two chunk buffers: chunk c lives in buffer c % 2 (NPER is even, so the parity carries across
+  // groups); a chunk's rows are read from LDS one step ahead, never held for the whole period, and the
+  // next chunk's DMA goes into the other buffer as soon as this one's has landed
+  static_assert(NPER % 2 == 0, "buffer = chunk parity across groups");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
-  auto issue_chunk = [&](int g, int c) __attribute__((always_inline)) {
+  auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < UNITS / kRegThreads; ++k) {
       const int unit = k * kRegThreads + lane;
       const int r = unit / n, j = unit % n;
       const int gb = g * BPG + r < nb ? g * BPG + r : nb - 1;
       __builtin_amdgcn_global_load_lds(in + (size_t)gb * block_bytes + (uint32_t)(c * n + j) * 16,
-                                       (lds_ptr_t)(lds + k * kRegThreads * 16), 16, 0, 0);
+                                       (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16), 16, 0, 0);
     }
   };
   const uint32_t row = (uint32_t)(uintptr_t)(lds_ptr_t)lds + (uint32_t)((lane / X::L) * ROWB);
@@ -831,7 +842,7 @@ void viterbi_multi_slot(RegArgs a, int ngroups) {
 
   uint32_t errors = 0;
   int g = blockIdx.x;
-  if (g < ngroups) issue_chunk(g, 0);
+  if (g < ngroups) issue_chunk(g, 0, 0);
   for (; g < ngroups; g += stride_groups) {
     const int blk = g * BPG + lane / X::L;
     const bool has_next = g + stride_groups < ngroups;
@@ -839,35 +850,33 @@ void viterbi_multi_slot(RegArgs a, int ngroups) {
 #pragma unroll
     for (int r = 0; r < 64; ++r) M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
     uint8_t info[IB];
-    // period p: the chunk's rows from LDS, the next chunk's DMA, eight phases
+    // period p: wait for the chunk's DMA, start the next one into the other buffer, eight phases
+    // reading each step's row one step ahead
     auto period_at = [&](int p, auto growth) __attribute__((always_inline)) {
       constexpr bool GROWTH = decltype(growth)::value;
-      f32x4 chunk[n];
       // this chunk's DMA was issued before the previous period's 8 decision stores (in order)
       if (p >= 2) wait_vmcnt<n>();
       else wait_vmcnt<0>();
-      [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
-        ((chunk[xs] = lds_read_b128<xs * 16>(row)), ...);
-      }(std::make_integer_sequence<int, n>{});
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(chunk[0]), "+v"(chunk[1]), "+v"(chunk[2]), "+v"(chunk[3]), "+v"(chunk[4]),
-                     "+v"(chunk[5]), "+v"(chunk[6]), "+v"(chunk[7])
-                   :
-                   : "memory");
       if constexpr (GROWTH) {
         const int bc = blk < nb ? blk : nb - 1;
 #pragma unroll
         for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
         asm volatile("" ::: "memory");   // info loads before the DMA (vmcnt order)
       }
-      if (p + 1 < NPER) issue_chunk(g, p + 1);
-      else issue_chunk(has_next ? g + stride_groups : g, 0);
+      const int buf = p & 1;
+      if (p + 1 < NPER) issue_chunk(g, p + 1, buf ^ 1);
+      else issue_chunk(has_next ? g + stride_groups : g, 0, buf ^ 1);
+      const uint32_t rd = row + (uint32_t)(buf * BUF);
+      f32x4 rowv = lds_read_b128<0>(rd);
       auto phase_at = [&]<int P>() __attribute__((always_inline)) {
-        const MT BM[4] = {chunk[P].x, chunk[P].y, chunk[P].z, chunk[P].w};
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rowv) :: "memory");
+        const MT BM[4] = {rowv.x, rowv.y, rowv.z, rowv.w};
+        if constexpr (P + 1 < n) rowv = lds_read_b128<(P + 1) * 16>(rd);
         if constexpr (GROWTH) {
           multi_growth_step_impl<C, P, false, MT, X>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
         } else {
-          const uint64_t w = multi_step<C, P, false, MT, X>(M, BM, qb0, qb1);
+          const uint64_t w = multi_step_impl<C, P, false, MT, X, CCV_SLOT_GROUP>(M, BM, qb0, qb1,
+                                                                               std::make_index_sequence<64>{});
           __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)w, (uint32_t)(w >> 32)}, slot, col,
                                                 ((p - 1) * n + P) * STEPB, 0);
         }

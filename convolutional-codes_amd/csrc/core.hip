@@ -758,8 +758,14 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
     a.park_flags = reinterpret_cast<uint8_t*>(base + hdr + met);
   }
   if (const char* env = std::getenv("CCV_FANO_COUNT_MOVES")) a.count_moves = env[0] == '1';
-  bool tab = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3);
-  if (const char* env = std::getenv("CCV_FANO_SYMTAB")) tab = tab && env[0] != '0';
+  // the expected-symbol table: hard input only. For soft input the table load sits in each move's
+  // dependent chain next to the row load, and the kernel waits on memory (PMC, round 4: wait 0.66 of
+  // wave time, valu_frac 0.17): the ~25 VALU of parities are cheaper (4 dB: 49.6 -> 57.7 Mbit/s, with
+  // the candidate rows prefetched 55.7 -> 67.2, profiles/r04c/fano_ab.txt). CCV_FANO_SYMTAB=0/1
+  // overrides.
+  bool tab = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3) && p->d.channel == CCV_HARD;
+  if (const char* env = std::getenv("CCV_FANO_SYMTAB"))
+    tab = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3) && env[0] != '0';
   if (tab) {
     if (ensure_symtab(p, stream)) return -1;
     a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);

@@ -1,9 +1,11 @@
 // reg_multi.hip -- ahead-of-time instantiation of the multi-lane register-trellis kernel
 // (acs_multi.hpp) for the K = 8 and K = 9 codes, soft and hard decision.
 #include <array>
+#include <cstdlib>
 #include <utility>
 
 #include "acs_multi.hpp"
+#include "acs_multi2.hpp"
 #include "acs_wide.hpp"
 #include "reg_codes.hpp"
 
@@ -50,6 +52,25 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence
   return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2) ? &launch_persist<I> : nullptr)...};
 }
 
+// The true-parity K = 9 slot kernel: two lanes per block (default) or four (CCV_K9_TRUE_LANES=4, A/B)
+inline bool k9_true_four_lanes() {
+  static const bool four = [] {
+    const char* env = std::getenv("CCV_K9_TRUE_LANES");
+    return env != nullptr && env[0] == '4';
+  }();
+  return four;
+}
+
+// The four-lane slot kernel's waves per SIMD: 3 (134 VGPRs) or 4 (CCV_K9_SLOT_WAVES=4: 128 VGPRs, a
+// few spills outside the main loop)
+inline int k9_slot_waves() {
+  static const int w = [] {
+    const char* env = std::getenv("CCV_K9_SLOT_WAVES");
+    return env != nullptr && env[0] == '4' ? 4 : 3;
+  }();
+  return w;
+}
+
 // Codes with a slot kernel (decisions through a per-wave scratch slot): K = 9 r = 1/2
 template <size_t I>
 constexpr bool has_slot_kernel() {
@@ -67,7 +88,14 @@ hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
     // true parity (256 distinct metrics): four lanes per block, the main periods as a loop with the
     // decisions through a per-wave slot, so the code fits the instruction cache (acs_multi.hpp
     // viterbi_multi_slot)
-    return launch_persistent(viterbi_multi_slot<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
+    // two lanes per block (acs_multi2.hpp); CCV_K9_TRUE_LANES=4: four lanes (acs_multi.hpp
+    // viterbi_multi_slot: 134 VGPRs, 3 waves per SIMD; a 4-wave build spills 15 VGPRs to scratch)
+    if (!k9_true_four_lanes())
+      return launch_persistent(viterbi_multi2_slot<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
+    else if (k9_slot_waves() == 4)
+      return launch_persistent(viterbi_multi_slot<kMultiCodes[I], kPersistBlen, 4>, a, ngroups, stream);
+    else
+      return launch_persistent(viterbi_multi_slot<kMultiCodes[I], kPersistBlen, 3>, a, ngroups, stream);
   else
     return hipErrorInvalidValue;
 }
@@ -78,21 +106,29 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_wide(std::index_sequence<I.
 }
 
 template <size_t I>
-constexpr size_t slot_bytes() {
+size_t slot_bytes() {
   if constexpr (!has_slot_kernel<I>()) return 0;
   else if constexpr (kMultiCodes[I].gen == GEN_REF_X86) return wide_slot_bytes<kMultiCodes[I], 2>(kPersistBlen);
-  else return multi_slot_bytes<kMultiCodes[I], kPersistBlen>();
+  else
+    return k9_true_four_lanes() ? multi_slot_bytes<kMultiCodes[I], kPersistBlen>()
+                                : multi2_slot_bytes<kMultiCodes[I], kPersistBlen>();
+}
+
+template <size_t I>
+int group_blocks() {
+  if constexpr (!has_slot_kernel<I>()) return 0;
+  else if constexpr (kMultiCodes[I].gen == GEN_REF_X86) return kRegThreads;   // one lane per block
+  else return k9_true_four_lanes() ? kRegThreads / 4 : kRegThreads / 2;
 }
 
 template <size_t... I>
-constexpr std::array<size_t, sizeof...(I)> make_slot_bytes(std::index_sequence<I...>) {
-  return {slot_bytes<I>()...};
+constexpr std::array<size_t (*)(), sizeof...(I)> make_slot_bytes(std::index_sequence<I...>) {
+  return {&slot_bytes<I>...};
 }
 
 template <size_t... I>
-constexpr std::array<int, sizeof...(I)> make_group_blocks(std::index_sequence<I...>) {
-  return {(!has_slot_kernel<I>() ? 0 : kMultiCodes[I].gen == GEN_REF_X86 ? kRegThreads
-                                                                         : kRegThreads / Multi<kMultiCodes[I]>::L)...};
+constexpr std::array<int (*)(), sizeof...(I)> make_group_blocks(std::index_sequence<I...>) {
+  return {&group_blocks<I>...};
 }
 
 constexpr auto kSoft = make<false>(std::make_index_sequence<kNumMultiCodes>{});
@@ -112,9 +148,9 @@ const RegLaunchFn* multi_persist_launchers() { return kSoftPersist.data(); }
 
 const RegLaunchFn* multi_wide_launchers() { return kSoftWide.data(); }
 
-size_t multi_wide_slot_bytes(int index) { return kSlotBytes[(size_t)index]; }
+size_t multi_wide_slot_bytes(int index) { return kSlotBytes[(size_t)index](); }
 
-int multi_wide_group_blocks(int index) { return kSlotGroupBlocks[(size_t)index]; }
+int multi_wide_group_blocks(int index) { return kSlotGroupBlocks[(size_t)index](); }
 
 const RegLaunchFn* multi_regdec_launchers(bool hard) {
   return hard ? kHardRegDec.data() : kSoftRegDec.data();

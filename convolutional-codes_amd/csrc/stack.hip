@@ -177,16 +177,18 @@ static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream
 }
 
 // Received rows (fano_dev.hpp, RM): in LDS for hard input (one byte per node, the footprint stays
-// small); for soft input read after the move (kRowsDirect). Measured at the bench size
-// (profiles/r01_fano.txt): soft K=15 rows in LDS (16 B per node) cut the chip from 9 to 2 waves per
-// CU and run 4x slower; prefetching the two candidate rows from global memory runs ~10 % slower --
-// under load the pass is bound by instruction issue, not by the row load. CCV_FANO_ROWS=0/1/2
+// small); for soft rate-1/2 input the two rows a move can land on are loaded from global memory at the
+// top of each pass (kRowsGlobal), so their latency overlaps the pass. Round 1 measured the prefetch
+// ~10 % slower (profiles/r01_fano.txt), but the round-3 one-loop kernel waits on memory (PMC, round 4:
+// wait 0.66, valu_frac 0.17) and the prefetch now wins: 4 dB 49.6 -> 55.7 Mbit/s, 67.2 with the
+// parities computed instead of the table load (profiles/r04c/fano_ab.txt). Soft K=15 rows in LDS
+// (16 B per node) cut the chip from 9 to 2 waves per CU and run 4x slower. CCV_FANO_ROWS=0/1/2
 // overrides.
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
   const size_t node_bytes = ((size_t)(a.T + 1) * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1) + 15) & ~(size_t)15;
   const size_t row_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : 16);
   const bool rowable = hard || (a.n == 2 && a.K <= 32);
-  int rm = hard ? kRowsLds : kRowsDirect;
+  int rm = hard ? kRowsLds : (rowable ? kRowsGlobal : kRowsDirect);
   if (const char* env = std::getenv("CCV_FANO_ROWS")) rm = rowable ? env[0] - '0' : kRowsDirect;
   if (rm == kRowsLds && node_bytes + row_bytes > 80 * 1024) rm = kRowsGlobal;
   if (rm < 0 || rm > 2) rm = kRowsDirect;
