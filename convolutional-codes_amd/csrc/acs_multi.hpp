@@ -159,6 +159,100 @@ __device__ __forceinline__ void multi_acs(MT (&M)[64], const MT (&BM)[1 << C.n],
   }
 }
 
+// ds_swizzle in quad-permute mode (lane i of each quad reads lane SEL[i] of it): the LDS unit's
+// crossbar, not a VALU instruction. On gfx950 a cross-lane VALU instruction (DPP, v_permlane*,
+// v_readlane) drops the wave's whole VALU stream to about half rate for the next ~1000 instructions:
+// a butterfly stream runs at 0.93-1.04 ns per instruction per SIMD, with 2 DPP adds per 1,605
+// instructions at 1.53, with one ds_swizzle or ds_bpermute per 402 at 0.93-0.97
+// (tools/raterbench7.hip, profiles/r04c/raterbench7.txt).
+template <int Q0, int Q1, int Q2, int Q3>
+__device__ __forceinline__ float swz_quad(float x) {
+  constexpr int pat = 0x8000 | (Q3 << 6) | (Q2 << 4) | (Q1 << 2) | Q0;
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), pat));
+}
+template <int Q0, int Q1, int Q2, int Q3>
+__device__ __forceinline__ uint32_t swz_quad_u32(uint32_t x) {
+  constexpr int pat = 0x8000 | (Q3 << 6) | (Q2 << 4) | (Q1 << 2) | Q0;
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, pat);
+}
+
+// Cross-lane phase P (X::is_lane(P)) of the four-lane slot kernel with the predecessors fetched by
+// ds_swizzle instead of DPP: registers in chunks of G, the swizzles of chunk c + 1 issued before the
+// ACS of chunk c so their LDS-unit latency overlaps it. Same values, same decision bits (register R
+// at bit R of hi:lo, descending) as multi_acs.
+template <CodeSpec C, int P, class X, int G = 8>
+__device__ __forceinline__ uint64_t multi_cross_swz(float (&M)[64], const float (&BM)[1 << C.n], bool qb0,
+                                                    bool qb1) {
+  static_assert(X::is_lane(P), "cross-lane phase");
+  constexpr int B = X::lane_of(P);
+  constexpr int L = X::L;
+  constexpr int NC = 64 / G;
+  float E[2][G], O[2][G];
+  auto issue = [&]<int c>() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int R = 63 - (c * G + i);
+      if constexpr (B == 0) {
+        E[c & 1][i] = swz_quad<0, 0, 2, 2>(M[R]);
+        O[c & 1][i] = swz_quad<1, 1, 3, 3>(M[R]);
+      } else {
+        E[c & 1][i] = swz_quad<0, 1, 0, 1>(M[R]);
+        O[c & 1][i] = swz_quad<2, 3, 2, 3>(M[R]);
+      }
+    }
+  };
+  uint32_t lo = 0, hi = 0;
+  auto compute = [&]<int c>() __attribute__((always_inline)) {
+    [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
+      ([&]() __attribute__((always_inline)) {
+        constexpr int R = 63 - (c * G + is);
+        constexpr auto e = [](int q, int odd) {
+          const int qe = q & ~(1 << B);
+          return expected_symbol(C, X::logical(qe, R, P) | (uint32_t)odd, (q >> B) & 1);
+        };
+        const float a0 = E[c & 1][is] + select_bm<L, e(0, 0), e(1 % L, 0), e(2 % L, 0), e(3 % L, 0)>(BM, qb0, qb1);
+        const float a1 = O[c & 1][is] + select_bm<L, e(0, 1), e(1 % L, 1), e(2 % L, 1), e(3 % L, 1)>(BM, qb0, qb1);
+        M[R] = vmin(a0, a1);
+        if constexpr (R >= 32) hi = shift_in(hi, a0, a1);
+        else lo = shift_in(lo, a0, a1);
+      }(), ...);
+    }(std::make_integer_sequence<int, G>{});
+  };
+  issue.template operator()<0>();
+  [&]<int... cs>(std::integer_sequence<int, cs...>) __attribute__((always_inline)) {
+    ([&]() __attribute__((always_inline)) {
+      if constexpr (cs + 1 < NC) issue.template operator()<cs + 1>();
+      __builtin_amdgcn_sched_barrier(0);
+      compute.template operator()<cs>();
+      __builtin_amdgcn_sched_barrier(0);
+    }(), ...);
+  }(std::make_integer_sequence<int, NC>{});
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Growth cross-lane phase through ds_swizzle (the slot kernel's XSWZ form of multi_growth): every
+// new state is its even predecessor, fetched from the pair's lane with the lane bit clear, plus the
+// branch metric.
+template <CodeSpec C, int P, class X>
+__device__ __forceinline__ void multi_growth_cross_swz(float (&M)[64], const float (&BM)[1 << C.n], bool qb0,
+                                                       bool qb1) {
+  static_assert(X::is_lane(P), "cross-lane phase");
+  constexpr int B = X::lane_of(P);
+  constexpr int L = X::L;
+  float E[64];
+#pragma unroll
+  for (int R = 0; R < 64; ++R) E[R] = B == 0 ? swz_quad<0, 0, 2, 2>(M[R]) : swz_quad<0, 1, 0, 1>(M[R]);
+  [&]<int... Rs>(std::integer_sequence<int, Rs...>) __attribute__((always_inline)) {
+    ([&]() __attribute__((always_inline)) {
+      constexpr auto e = [](int q) {
+        const int qe = q & ~(1 << B);
+        return expected_symbol(C, X::logical(qe, Rs, P), (q >> B) & 1);
+      };
+      M[Rs] = E[Rs] + select_bm<L, e(0), e(1 % L), e(2 % L), e(3 % L)>(BM, qb0, qb1);
+    }(), ...);
+  }(std::make_integer_sequence<int, 64>{});
+}
+
 // Growth step (t = P < K-1, from the reset metrics): the odd predecessor of every state is still
 // unreachable (its candidate is +inf / saturated 0xFF00 and never wins the strict compare), so each
 // new state is its even predecessor plus the branch metric and its decision is 0 -- the adds only
@@ -790,7 +884,7 @@ constexpr size_t multi_slot_bytes() {
 #ifndef CCV_SLOT_GROUP
 #define CCV_SLOT_GROUP 0
 #endif
-template <CodeSpec C, int BLEN, int WAVES = 3, int LB0 = 0, int LB1 = 3>
+template <CodeSpec C, int BLEN, int WAVES = 3, bool XSWZ = false, int LB0 = 0, int LB1 = 3>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(WAVES)))
 void viterbi_multi_slot(RegArgs a, int ngroups) {
   using X = Multi<C, LB0, LB1>;
@@ -873,10 +967,16 @@ void viterbi_multi_slot(RegArgs a, int ngroups) {
         const MT BM[4] = {rowv.x, rowv.y, rowv.z, rowv.w};
         if constexpr (P + 1 < n) rowv = lds_read_b128<(P + 1) * 16>(rd);
         if constexpr (GROWTH) {
-          multi_growth_step_impl<C, P, false, MT, X>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
+          if constexpr (X::is_lane(P) && XSWZ)
+            multi_growth_cross_swz<C, P, X>(M, BM, qb0, qb1);
+          else
+            multi_growth_step_impl<C, P, false, MT, X>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
         } else {
-          const uint64_t w = multi_step_impl<C, P, false, MT, X, CCV_SLOT_GROUP>(M, BM, qb0, qb1,
-                                                                               std::make_index_sequence<64>{});
+          uint64_t w;
+          if constexpr (X::is_lane(P) && XSWZ)   // cross-lane phase through the LDS crossbar
+            w = multi_cross_swz<C, P, X>(M, BM, qb0, qb1);
+          else
+            w = multi_step_impl<C, P, false, MT, X, CCV_SLOT_GROUP>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
           __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)w, (uint32_t)(w >> 32)}, slot, col,
                                                 ((p - 1) * n + P) * STEPB, 0);
         }
@@ -925,8 +1025,13 @@ void viterbi_multi_slot(RegArgs a, int ngroups) {
           else pos = multi_dec_pos_k(rl, X::reg_bit(P));
           const uint32_t own = (uint32_t)(dw[pp & 1][P] >> pos) & 1u;
           uint32_t m = own << qself;
-          m |= dpp_u32<0xB1>(m);   // quad_perm [1,0,3,2]
-          m |= dpp_u32<0x4E>(m);   // quad_perm [2,3,0,1]
+          if constexpr (XSWZ) {   // through the LDS crossbar (no cross-lane VALU, see swz_quad)
+            m |= swz_quad_u32<1, 0, 3, 2>(m);
+            m |= swz_quad_u32<2, 3, 0, 1>(m);
+          } else {
+            m |= dpp_u32<0xB1>(m);   // quad_perm [1,0,3,2]
+            m |= dpp_u32<0x4E>(m);   // quad_perm [2,3,0,1]
+          }
           const uint32_t d = (m >> ql) & 1u;
           if constexpr (X::is_lane(P)) {
             constexpr uint32_t bit = 1u << X::lane_of(P);

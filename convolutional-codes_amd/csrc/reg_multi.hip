@@ -52,11 +52,11 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence
   return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2) ? &launch_persist<I> : nullptr)...};
 }
 
-// The true-parity K = 9 slot kernel: two lanes per block (default) or four (CCV_K9_TRUE_LANES=4, A/B)
+// The true-parity K = 9 slot kernel: four lanes per block (default) or two (CCV_K9_TRUE_LANES=2, A/B)
 inline bool k9_true_four_lanes() {
   static const bool four = [] {
     const char* env = std::getenv("CCV_K9_TRUE_LANES");
-    return env != nullptr && env[0] == '4';
+    return env == nullptr || env[0] != '2';
   }();
   return four;
 }
@@ -69,6 +69,15 @@ inline int k9_slot_waves() {
     return env != nullptr && env[0] == '4' ? 4 : 3;
   }();
   return w;
+}
+
+// the four-lane slot kernel's cross-lane phases through ds_swizzle (default) or DPP (CCV_K9_SLOT_XSWZ=0)
+inline bool k9_slot_xswz() {
+  static const bool v = [] {
+    const char* env = std::getenv("CCV_K9_SLOT_XSWZ");
+    return env == nullptr || env[0] != '0';
+  }();
+  return v;
 }
 
 // Codes with a slot kernel (decisions through a per-wave scratch slot): K = 9 r = 1/2
@@ -90,8 +99,13 @@ hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
     // viterbi_multi_slot)
     // two lanes per block (acs_multi2.hpp); CCV_K9_TRUE_LANES=4: four lanes (acs_multi.hpp
     // viterbi_multi_slot: 134 VGPRs, 3 waves per SIMD; a 4-wave build spills 15 VGPRs to scratch)
+    // four lanes per block, cross-lane phases through ds_swizzle (production: 34.1 Gbit/s at 32
+    // frames); A/B forms: CCV_K9_SLOT_XSWZ=0 the same kernel with DPP adds (27.9; 4 waves per SIMD
+    // with CCV_K9_SLOT_WAVES=4: 27.7), CCV_K9_TRUE_LANES=2 two lanes per block with DPP (27.5)
     if (!k9_true_four_lanes())
       return launch_persistent(viterbi_multi2_slot<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
+    else if (k9_slot_xswz())
+      return launch_persistent(viterbi_multi_slot<kMultiCodes[I], kPersistBlen, 3, true>, a, ngroups, stream);
     else if (k9_slot_waves() == 4)
       return launch_persistent(viterbi_multi_slot<kMultiCodes[I], kPersistBlen, 4>, a, ngroups, stream);
     else

@@ -340,12 +340,66 @@ CCV_ROW_FN2(row_min_min_u32, uint32_t, uint32_t, "v_min_u32", "v_min_u32")
 #undef CCV_ROW_REDUCE2
 #undef CCV_ROW_STEP2
 
+
+
 // max / min without the canonicalising v_max x,x hipcc wraps around fmaxf (IEEE max/min skip NaN,
 // as the reference's strict compares do)
 __device__ __forceinline__ float vmax2(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
 __device__ __forceinline__ float vmin2(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
 __device__ __forceinline__ int32_t vmax2(int32_t a, int32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ int32_t vmin2(int32_t a, int32_t b) { return a < b ? a : b; }
+
+// The same pair of row reductions through the LDS crossbar (ds_swizzle, bit mode: lane ^ m within 32
+// lanes, m = 1, 2, 4, 8), with no cross-lane VALU instruction -- which on gfx950 drops a wave's whole
+// VALU stream to about half rate for the next ~1000 instructions (tools/raterbench7.hip,
+// profiles/r04c/raterbench7.txt). NOT the default: the stack search is latency-bound, and the
+// swizzles' LDS-unit round trips in the iteration's dependent chain cost more than the halved VALU
+// rate (round 4 A/B: soft 587 -> 445, BSC 1285 -> 1074 Mbit/s). CCV_STACK_SWZ=1 at build time.
+#ifndef CCV_STACK_SWZ
+#define CCV_STACK_SWZ 0
+#endif
+template <int M>
+__device__ __forceinline__ int32_t swz_xor(int32_t v) {
+  return __builtin_amdgcn_ds_swizzle(v, (M << 10) | 0x1F);   // and 0x1F, or 0, xor M
+}
+template <int RL, class F>
+__device__ __forceinline__ void row_pair_swz(uint32_t& a, uint32_t& b, F&& combine) {
+  auto step = [&]<int M>() __attribute__((always_inline)) {
+    const uint32_t ta = (uint32_t)swz_xor<M>((int32_t)a), tb = (uint32_t)swz_xor<M>((int32_t)b);
+    combine(a, b, ta, tb);
+  };
+  step.template operator()<1>();
+  step.template operator()<2>();
+  step.template operator()<4>();
+  if constexpr (RL == 16) step.template operator()<8>();
+}
+template <int RL>
+__device__ __forceinline__ void row_max_min_swz(float& a, float& b) {
+  uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+  row_pair_swz<RL>(ua, ub, [](uint32_t& x, uint32_t& y, uint32_t tx, uint32_t ty) {
+    x = __float_as_uint(vmax2(__uint_as_float(x), __uint_as_float(tx)));
+    y = __float_as_uint(vmin2(__uint_as_float(y), __uint_as_float(ty)));
+  });
+  a = __uint_as_float(ua);
+  b = __uint_as_float(ub);
+}
+template <int RL>
+__device__ __forceinline__ void row_max_min_swz(int32_t& a, int32_t& b) {
+  uint32_t ua = (uint32_t)a, ub = (uint32_t)b;
+  row_pair_swz<RL>(ua, ub, [](uint32_t& x, uint32_t& y, uint32_t tx, uint32_t ty) {
+    x = (uint32_t)vmax2((int32_t)x, (int32_t)tx);
+    y = (uint32_t)vmin2((int32_t)y, (int32_t)ty);
+  });
+  a = (int32_t)ua;
+  b = (int32_t)ub;
+}
+template <int RL>
+__device__ __forceinline__ void row_min_min_u32_swz(uint32_t& a, uint32_t& b) {
+  row_pair_swz<RL>(a, b, [](uint32_t& x, uint32_t& y, uint32_t tx, uint32_t ty) {
+    x = tx < x ? tx : x;
+    y = ty < y ? ty : y;
+  });
+}
 
 // LDS bytes per row: the block's symbols (16-byte aligned), 65 entry records (64 + a dummy), then
 // the 64 path metrics + the dummy (padded to 68)
@@ -463,7 +517,8 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
           kx = vmax2(kx, (int32_t)((uint32_t)met[k] * 64u) + (63 - (l * kRowSlots + k)));
           kn = vmin2(kn, (int32_t)((uint32_t)met[k] * 64u) + (l * kRowSlots + k));
         }
-        row_max_min<RL>(kx, kn);
+        if constexpr (CCV_STACK_SWZ) row_max_min_swz<RL>(kx, kn);
+        else row_max_min<RL>(kx, kn);
         mx = (MT)(kx >> 6);
         cur = 63u - ((uint32_t)kx & 63u);
         ok = kx > -(1 << 30);
@@ -477,7 +532,8 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
           mx = vmax2(mx, met[k]);
           mn = vmin2(mn, met[k]);
         }
-        row_max_min<RL>(mx, mn);
+        if constexpr (CCV_STACK_SWZ) row_max_min_swz<RL>(mx, mn);
+        else row_max_min<RL>(mx, mn);
         uint32_t cand = kStackDepth;
         c2 = kStackDepth;
 #pragma unroll
@@ -485,7 +541,8 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
           cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
           c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
         }
-        row_min_min_u32<RL>(cand, c2);
+        if constexpr (CCV_STACK_SWZ) row_min_min_u32_swz<RL>(cand, c2);
+        else row_min_min_u32<RL>(cand, c2);
         cur = cand;
         ok = mx > lo_sent;
       }

@@ -44,6 +44,48 @@ K(k_bfsel, BF2 BF2 SEL4)                // butterflies with per-lane selects: 44
 K(k_xp, XP4)                            // 28
 #define BF8 BF2 BF2 BF2 BF2
 K(k_sparse, BF8 BF8 BF8 BF8 BF8 XS("v4", "v8", "v9", "v12", "v16"))   // 400 + 5: 2 DPP per 405
+#define BF40 BF8 BF8 BF8 BF8 BF8
+K(k_sparse1600, BF40 BF40 BF40 BF40 XS("v4", "v8", "v9", "v12", "v16"))   // 1600 + 5
+// the same density with cross-lane moves through the LDS unit or the scalar unit instead of DPP
+#define SWZ(m) "ds_swizzle_b32 v26, " m " offset:swizzle(QUAD_PERM,1,0,3,2)\n"
+#define BPM(m) "ds_bpermute_b32 v27, v30, " m "\n"
+#define RDL(m) "v_readlane_b32 s4, " m ", 5\n"
+K(k_swz, BF40 SWZ("v4") "s_waitcnt lgkmcnt(0)\n")    // 400 + 2
+K(k_bpm, BF40 BPM("v4") "s_waitcnt lgkmcnt(0)\n")    // 400 + 2
+K(k_rdl, BF40 RDL("v4"))                             // 400 + 1
+K(k_swz8, BF2 BF2 SWZ("v4") SWZ("v5") SWZ("v6") SWZ("v7") "s_waitcnt lgkmcnt(0)\n")   // 40 + 5
+// one cross-lane instruction at the START of the kernel only, then the plain butterfly stream
+__global__ __launch_bounds__(256) void k_rfl_start(float* o, int it) {
+  asm volatile("v_readfirstlane_b32 s4, v4" ::: "s4");
+  for (int i = 0; i < it; ++i) asm volatile(R8(BF2 BF2) ::: CLOB);
+  if (it < 0) o[0] = 0;
+}
+__global__ __launch_bounds__(256) void k_dpp_start(float* o, int it) {
+  asm volatile("v_add_f32_dpp v8, v4, v20 quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" ::: "v8");
+  for (int i = 0; i < it; ++i) asm volatile(R8(BF2 BF2) ::: CLOB);
+  if (it < 0) o[0] = 0;
+}
+// the K = 7 persistent kernel's other instructions at its density (one 8-step chunk = ~1,600 VALU):
+// 8 ds_read_b128 of the chunk rows and 8 LDS-DMA loads of the next chunk, per 1,600 VALU
+__global__ __launch_bounds__(256) void k_bf_lds(float* o, int it) {
+  __shared__ float4 buf[2048];
+  const unsigned addr = (unsigned)(uintptr_t)buf + (threadIdx.x & 63) * 16;
+  for (int i = 0; i < it; ++i) {
+    asm volatile(R8(BF40 "ds_read_b128 v[26:29], %0\n") "s_waitcnt lgkmcnt(0)\n" :: "v"(addr) : CLOB);
+  }
+  if (it < 0) o[0] = buf[threadIdx.x].x;
+}
+__global__ __launch_bounds__(256) void k_bf_dma(float* o, int it) {
+  __shared__ float4 buf[4096];
+  const float* src = o + (threadIdx.x & 63) * 4;
+  for (int i = 0; i < it; ++i) {
+    for (int k = 0; k < 8; ++k)
+      __builtin_amdgcn_global_load_lds(src + k * 256, (__attribute__((address_space(3))) void*)(buf + (threadIdx.x / 64) * 512 + k * 64), 16, 0, 0);
+    asm volatile(R8(BF40) ::: CLOB);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (it < 0) o[0] = buf[threadIdx.x].x;
+}
 // a DPP add in a branch that never executes at run time (it < 0): a kernel that CONTAINS DPP
 __global__ __launch_bounds__(256) void k_dead_dpp(float* o, int it) {
   for (int i = 0; i < it; ++i) {
@@ -54,14 +96,19 @@ __global__ __launch_bounds__(256) void k_dead_dpp(float* o, int it) {
 }
 K(k_mix1of8p, BF2 BF2 BF2 BF2 BF2 BF2 BF2 XP4 XP4)   // 140 + 56
 int main() {
-  float* d; (void)hipMalloc(&d, 4096);
+  float* d; (void)hipMalloc(&d, 1 << 20);
   hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
   struct { const char* n; void (*k)(float*, int); double per; } ks[] = {
     {"butterflies (4 add 2 sub 2 min 2 alignbit)", k_bf, 40}, {"cross states, 2 DPP adds", k_xs, 20},
     {"cross states, DPP mov + 2 adds", k_xm, 24}, {"mix 7 in-lane : 1 cross (DPP adds)", k_mix1of8, 180},
     {"mix 6 in-lane : 2 cross (DPP adds)", k_mix2of8, 100}, {"butterflies + 10% cndmask_e64", k_bfsel, 44},
     {"cross states, mov + permlane32_swap + 2 adds", k_xp, 28}, {"mix 7 in-lane : 1 cross (permlane32)", k_mix1of8p, 196},
-    {"butterflies + 2 DPP adds per 405 instructions", k_sparse, 405}, {"butterflies, DPP code never executed", k_dead_dpp, 40}};
+    {"butterflies + 2 DPP adds per 405 instructions", k_sparse, 405}, {"butterflies, DPP code never executed", k_dead_dpp, 40},
+    {"butterflies + 2 DPP adds per 1605 instructions", k_sparse1600, 1605}, {"butterflies + 1 ds_swizzle per 402", k_swz, 402},
+    {"butterflies + 1 ds_bpermute per 402", k_bpm, 402}, {"butterflies + 1 v_readlane per 401", k_rdl, 401},
+    {"butterflies + 4 ds_swizzle per 45", k_swz8, 45}, {"butterflies, one v_readfirstlane at kernel start", k_rfl_start, 40},
+    {"butterflies, one DPP add at kernel start", k_dpp_start, 40},
+    {"butterflies + 1 ds_read_b128 per 400", k_bf_lds, 401}, {"butterflies + 8 LDS-DMA per 3,200", k_bf_dma, 400}};
   const int it = 200, blocks = 256 * 4;
   for (int rep = 0; rep < 2; ++rep)
     for (auto& k : ks) {
