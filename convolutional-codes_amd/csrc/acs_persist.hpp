@@ -273,7 +273,8 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
              kPersistDepth2 = 16, kPersistLineChunks = 32, kPersistNoMemRandom = 64,
-             kPersistNoDma = 128, kPersistNoLdsRead = 256, kPersistInputNt = 512, kPersistTwins = 1024 };
+             kPersistNoDma = 128, kPersistNoLdsRead = 256, kPersistInputNt = 512, kPersistTwins = 1024,
+             kPersistStage = 2048 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -302,6 +303,15 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   // not the production path.
   constexpr bool LINES = (T % PF) != 0 && (ABLATE & kPersistLineChunks) != 0 && (ABLATE & kPersistNoMem) == 0;
   constexpr bool DEPTH2 = !LINES && (ABLATE & kPersistDepth2) != 0;   // two chunks in flight
+  // STAGE: no LDS-DMA. A global_load_lds instruction holds the SIMD's VALU issue: 8 of them per 3,200
+  // butterfly instructions cost the stream 25 %, 16 cost 49 %, while 8 coalesced global_load_dwordx4
+  // into VGPRs cost nothing (tools/raterbench7.hip, profiles/r04c/raterbench7f.txt) -- and this kernel
+  // issues 8 per 8-step chunk (~1,600 VALU). So the chunk's 16-byte units (the DMA's unit mapping) are
+  // loaded into VGPRs at the chunk's first step, written to the other LDS buffer at its fifth (after
+  // vmcnt(0)) with ds_write_b128, and every step reads its row one step ahead. (Each lane loading its
+  // own block's rows instead -- 64 lines per instruction -- ran 0.61x: the address processing of the
+  // scattered loads stalls issue, round-4 A/B.)
+  constexpr bool STAGE = (ABLATE & kPersistStage) != 0 && !LINES && !DEPTH2 && (ABLATE & kPersistNoMem) == 0;
   constexpr int NLINE = NCH + 1;              // aligned lines per block window sequence (LINES)
   using DW = DecWord<S>;
   const int lane = threadIdx.x;
@@ -309,7 +319,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   const int stride_groups = gridDim.x;
 
   __shared__ __attribute__((aligned(1024))) unsigned char
-      lds[(LINES || DEPTH2) ? 2 * BUF : BUF];
+      lds[(LINES || DEPTH2 || STAGE) ? 2 * BUF : BUF];
   // kPersistTwins (A/B, not the production path): one decision per value-numbering class of the
   // x86-idiom K = 7 code (twins.hpp) -- 3.7 % fewer VALU, but the traceback's state -> (word, bit)
   // lookup in LDS lengthens its dependent chain: 1.02x the time (profiles/r03_k7_twin_ab.txt)
@@ -400,10 +410,49 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   const uint32_t rd_base = (uint32_t)(uintptr_t)(lds_ptr_t)lds + (uint32_t)(lane * ROWB) +
                            (uint32_t)(((lane / GRP) % UPR) * 16);
 
+  // STAGE: the input as one buffer resource (byte offsets < 2^31: the host splits larger batches)
+  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(in), 0,
+      (int)((size_t)nb * block_bytes < 0x7FFFFFFFu ? (size_t)nb * block_bytes : 0x7FFFFFFFu), 0x00020000);
+  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+  u32x4s stg[UPR];
+  // chunk c of group gg into stg (unit k = the DMA's unit k); the group holding the batch's last
+  // block clamps each unit into the buffer, as issue_chunk does
+  auto load_chunk = [&](int gg, int c) __attribute__((always_inline)) {
+    if (gg * kRegThreads + kRegThreads < nb) {
+      const int soff = gg * kRegThreads * (int)block_bytes + c * PF * 16;
+#pragma unroll
+      for (int k = 0; k < UPR; ++k) stg[k] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, dma_off[k], soff, 0);
+    } else {
+#pragma unroll
+      for (int k = 0; k < UPR; ++k) {
+        const int r = k * (kRegThreads / UPR) + lane / UPR, j = lane % UPR;
+        const int su = j ^ ((r / GRP) % UPR);
+        const int gb = gg * kRegThreads + r < nb ? gg * kRegThreads + r : nb - 1;
+        uint32_t off = (uint32_t)(c * PF + su) * 16;
+        off = off < block_bytes ? off : block_bytes - 16;
+        stg[k] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, (uint32_t)gb * block_bytes + off, 0, 0);
+      }
+    }
+  };
+  auto store_chunk = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < UPR; ++k)
+      *reinterpret_cast<u32x4s*>(lds + buf * BUF + (k * kRegThreads + lane) * 16) = stg[k];
+    asm volatile("" ::: "memory");   // before any later LDS read (the reads are asm)
+  };
+
   uint32_t errors = 0;
   int g = blockIdx.x;
   uint32_t gp = 0;   // LINES: buffer of the group's line 0 (flips per group: NLINE is odd)
-  if (!(ABLATE & kPersistNoMem) && g < ngroups) {
+  if constexpr (STAGE) {
+    if (g < ngroups) {
+      load_chunk(g, 0);
+      wait_vmcnt<0>();
+      store_chunk(0);
+    }
+  }
+  if (!(ABLATE & kPersistNoMem) && !STAGE && g < ngroups) {
     if constexpr (LINES) {
       issue_line(g, 0, 0);
       issue_line(g, 1, 1);
@@ -436,7 +485,19 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
                            __uint_as_float((r0 & 0x7FFFFFu) | 0x3F800000u), __uint_as_float((r1 & 0x7FFFFFu) | 0x3F800000u)};
         }
       };
-      if constexpr ((ABLATE & kPersistNoMemRandom) != 0) {   // no memory, full-entropy values
+      f32x4 rowv{};
+      if constexpr (STAGE) {
+        // this chunk's rows were written to buffer c & 1 during the previous chunk
+        if constexpr (c == 0) {
+          const int bc = b < nb ? b : nb - 1;
+#pragma unroll
+          for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
+          asm volatile("" ::: "memory");
+        }
+        if constexpr (c + 1 < NCH) load_chunk(g, c + 1);
+        else load_chunk(has_next ? g + stride_groups : g, 0);
+        rowv = lds_read_b128<(c & 1) * BUF>(rd_base);
+      } else if constexpr ((ABLATE & kPersistNoMemRandom) != 0) {   // no memory, full-entropy values
         synth_rows();
       } else if constexpr ((ABLATE & kPersistNoMem) != 0) {
         int ln = lane + g;
@@ -510,6 +571,15 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
       }
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
         constexpr int t = c * PF + u;
+        if constexpr (STAGE) {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rowv) :: "memory");
+          chunk[u] = rowv;
+          if constexpr (u + 1 < PF) rowv = lds_read_b128<(c & 1) * BUF>(rd_base ^ (uint32_t)((u + 1) * 16));
+          if constexpr (u == PF / 2) {   // the next chunk's units have landed: into the other buffer
+            wait_vmcnt<0>();
+            store_chunk((c + 1) & 1);
+          }
+        }
         const float bm[4] = {chunk[u].x, chunk[u].y, chunk[u].z, chunk[u].w};
         if constexpr (t < G) growth_step<C, t, float>(M, bm, __builtin_inff());
         else if constexpr (t < T) {
@@ -544,8 +614,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
       uint64_t ref = 0;
 #pragma unroll
       for (int k = 0; k < IB; ++k) ref |= (uint64_t)info[k] << (56 - 8 * k);
-      // exactly OB byte stores per group (the vmcnt arithmetic above counts them); lanes past the
-      // batch store nothing (exec-masked)
+      // lanes past the batch store nothing (exec-masked)
       if (b < nb) {
         uint8_t* o = a.out + (size_t)b * OB;
 #pragma unroll

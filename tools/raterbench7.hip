@@ -86,6 +86,35 @@ __global__ __launch_bounds__(256) void k_bf_dma(float* o, int it) {
   }
   if (it < 0) o[0] = buf[threadIdx.x].x;
 }
+template <int NDMA, bool WAIT>
+__global__ __launch_bounds__(256) void k_bf_dma_v(float* o, int it) {
+  __shared__ float4 buf[4096];
+  const float* src = o + (threadIdx.x & 63) * 4;
+  for (int i = 0; i < it; ++i) {
+    for (int k = 0; k < NDMA; ++k)
+      __builtin_amdgcn_global_load_lds(src + k * 256, (__attribute__((address_space(3))) void*)(buf + (threadIdx.x / 64) * 512 + k * 64), 16, 0, 0);
+    asm volatile(R8(BF40) ::: CLOB);
+    if (WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (it < 0) o[0] = buf[threadIdx.x].x;
+}
+// plain global loads into VGPRs at the same density (the data is consumed by an empty asm)
+template <int NL>
+__global__ __launch_bounds__(256) void k_bf_gload(float* o, int it) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const f4* src = reinterpret_cast<const f4*>(o) + (threadIdx.x & 63);
+  f4 acc = {0, 0, 0, 0};
+  for (int i = 0; i < it; ++i) {
+    f4 v[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) v[k] = src[k * 64 + (i & 1)];
+    asm volatile(R8(BF40) ::: CLOB);
+#pragma unroll
+    for (int k = 0; k < NL; ++k) asm volatile("" :: "v"(v[k]));
+  }
+  if (it < 0) o[0] = acc.x;
+}
 // a DPP add in a branch that never executes at run time (it < 0): a kernel that CONTAINS DPP
 __global__ __launch_bounds__(256) void k_dead_dpp(float* o, int it) {
   for (int i = 0; i < it; ++i) {
@@ -108,7 +137,11 @@ int main() {
     {"butterflies + 1 ds_bpermute per 402", k_bpm, 402}, {"butterflies + 1 v_readlane per 401", k_rdl, 401},
     {"butterflies + 4 ds_swizzle per 45", k_swz8, 45}, {"butterflies, one v_readfirstlane at kernel start", k_rfl_start, 40},
     {"butterflies, one DPP add at kernel start", k_dpp_start, 40},
-    {"butterflies + 1 ds_read_b128 per 400", k_bf_lds, 401}, {"butterflies + 8 LDS-DMA per 3,200", k_bf_dma, 400}};
+    {"butterflies + 1 ds_read_b128 per 400", k_bf_lds, 401}, {"butterflies + 8 LDS-DMA per 3,200", k_bf_dma, 400},
+    {"butterflies + 8 LDS-DMA per 3,200, no wait", k_bf_dma_v<8, false>, 400},
+    {"butterflies + 1 LDS-DMA per 3,200", k_bf_dma_v<1, true>, 400},
+    {"butterflies + 16 LDS-DMA per 3,200", k_bf_dma_v<16, true>, 400},
+    {"butterflies + 8 global_load_dwordx4 per 3,200", k_bf_gload<8>, 400}};
   const int it = 200, blocks = 256 * 4;
   for (int rep = 0; rep < 2; ++rep)
     for (auto& k : ks) {
