@@ -665,15 +665,29 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
   constexpr int kBuf = kRegThreads * kHardPersistMaxT;
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kBuf];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
-  constexpr int units = (kRegThreads * T) >> 2;   // dwords per group (64 * T is a multiple of 4)
+  // 16-byte DMA units (round 4; dword units before): an LDS-DMA instruction holds the SIMD's VALU
+  // issue whatever its width (tools/raterbench7.hip), so the group moves in 3
+  // instructions instead of 12 at T = 46. The LDS image is the same: the group's bytes, contiguous.
+  constexpr int units = (kRegThreads * T + 15) >> 4;   // 16-byte units per group
   auto issue_group = [&](int g, int buf) __attribute__((always_inline)) {
     const unsigned char* src = in + (size_t)g * kRegThreads * T;
+    if constexpr ((kRegThreads * T) % 16 == 0) {
 #pragma unroll
-    for (int k = 0; k * kRegThreads < units; ++k) {
-      int u = k * kRegThreads + lane;
-      u = u < units ? u : units - 1;   // past the group: clamped (LDS slot never read)
-      __builtin_amdgcn_global_load_lds(src + (size_t)u * 4, (lds_ptr_t)(lds + buf * kBuf + k * kRegThreads * 4),
-                                       4, 0, 0);
+      for (int k = 0; k * kRegThreads < units; ++k) {
+        int u = k * kRegThreads + lane;
+        u = u < units ? u : units - 1;   // past the group: clamped (LDS slot never read)
+        __builtin_amdgcn_global_load_lds(src + (size_t)u * 16, (lds_ptr_t)(lds + buf * kBuf + k * kRegThreads * 16),
+                                         16, 0, 0);
+      }
+    } else {   // 64 * T not a multiple of 16: dword units
+      constexpr int dunits = (kRegThreads * T) >> 2;
+#pragma unroll
+      for (int k = 0; k * kRegThreads < dunits; ++k) {
+        int u = k * kRegThreads + lane;
+        u = u < dunits ? u : dunits - 1;
+        __builtin_amdgcn_global_load_lds(src + (size_t)u * 4, (lds_ptr_t)(lds + buf * kBuf + k * kRegThreads * 4),
+                                         4, 0, 0);
+      }
     }
   };
 

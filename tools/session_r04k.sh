@@ -16,4 +16,7 @@ import json; d=json.loads(open('gpurun_out/k7t_d$v.log').read().strip().splitlin
 print('k7:true stage=$v', d['value'], d['kernel_ms'], d['ber']['errors'])"
 done
 CCV_PERSIST_STAGE=1 bash tools/pmc_workload.sh > gpurun_out/pmc_k7stage.log 2>&1 || exit 1
+
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "bsc or hard" -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_hard.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_hard.log; [ $rc -ne 0 ] && exit $rc
+TAG=bsc bash tools/ab_bench.sh "--channel bsc" head r04c || exit 1
 echo done
