@@ -877,6 +877,48 @@ def test_device_channel_k9_frames_path_equals_fused(torch_cuda, gen):
         assert a[4] == b[4]
 
 
+def _frames_only_plans():
+    from ccviterbi import K15, FanoPlan, StackPlan
+    return [("viterbi_k7", Plan, K7), ("viterbi_code5_r13", Plan, CODEBOOK[5]),
+            ("stack_k15", StackPlan, K15), ("stack_k15_true", StackPlan, K15.with_(gen_mode=GEN_TRUE_PARITY)),
+            ("stack_wspr", StackPlan, CODEBOOK[4]), ("fano_k15", FanoPlan, K15),
+            ("stack_k15_blen200", StackPlan, K15.with_(blen=200))]
+
+
+@pytest.mark.parametrize("idx", range(7), ids=[p[0] for p in _frames_only_plans()])
+@pytest.mark.parametrize("channel", [SOFT, HARD])
+def test_device_channel_frames_only(torch_cuda, idx, channel):
+    """CCV_CHANNEL_FRAMES_ONLY (the producer of the stack / Fano device sweeps, any K <= 32): info
+    bytes and decoder input from the run-time-code encoder equal the host Philox producer's
+    (BSC bit-exact; AWGN within the libm tolerance of test_device_channel_awgn), ragged counts,
+    first_block offsets, and the hard demapper on AWGN."""
+    name, cls, c = _frames_only_plans()[idx]
+    plan = cls(c, channel)
+    for nb, first, demap in ((1, 0, False), (333, 123456, False), (70, 99, channel == SOFT)):
+        shape = (nb, c.steps) if channel == HARD else (nb, c.steps, 1 << c.n)
+        d_ch = torch_cuda.empty(shape, dtype=torch_cuda.uint8 if channel == HARD else torch_cuda.float32,
+                                device="cuda")
+        d_info = torch_cuda.empty((nb, c.info_bytes), dtype=torch_cuda.uint8, device="cuda")
+        if channel == HARD:
+            plan.simulate_frames(41, first, nb, 80000, d_ch, d_info=d_info)
+            h_info, h_rx = ch.bsc_blocks(c, nb, 80000, 41, first_block=first)
+        else:
+            s = ch.noise_scaling(2.5)
+            plan.simulate_frames(41, first, nb, s, d_ch, d_info=d_info, hard_demap=demap)
+            h_info, h_rx = ch.awgn_blocks(c, nb, s, 41, first_block=first, hard_demap=demap)
+        torch_cuda.cuda.synchronize()
+        info, rx = d_info.cpu().numpy(), d_ch.cpu().numpy()
+        assert np.array_equal(info, h_info)
+        if channel == HARD:
+            assert np.array_equal(rx, h_rx)
+        elif demap:
+            assert np.mean(np.all(rx == h_rx, axis=2)) >= 0.999
+        else:
+            assert np.mean(rx == h_rx) >= 0.999
+            assert np.allclose(rx, h_rx, rtol=1e-5, atol=1e-6)
+    plan.close()
+
+
 @pytest.mark.parametrize("channel", [SOFT, HARD])
 def test_device_channel_lds_vs_hbm_decisions(torch_cuda, channel):
     """The LDS-decision channel kernel (CCV_CHANNEL_LDS_DECISIONS=1, the BSC default) and the

@@ -18,5 +18,6 @@ done
 CCV_PERSIST_STAGE=1 bash tools/pmc_workload.sh > gpurun_out/pmc_k7stage.log 2>&1 || exit 1
 
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "bsc or hard" -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_hard.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_hard.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "frames_only" -x -q --timeout 100 --timeout-method thread > gpurun_out/pytest_frames.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_frames.log; [ $rc -ne 0 ] && exit $rc
 TAG=bsc bash tools/ab_bench.sh "--channel bsc" head r04c || exit 1
 echo done
