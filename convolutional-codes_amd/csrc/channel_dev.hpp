@@ -10,8 +10,8 @@
 //   half first, u1 == 0 redrawn); common/demapper.c:61-70 (squared distance / ndist in fp32);
 //   binary-symmetric-channel/main.c:57-72 (per bit: rand() % 1000000 < p_ppm flips it).
 // Info bits, symbols and BSC flips are bit-identical to the host producer. The AWGN samples use the
-// device libm (ocml) log/sin/cos instead of glibc's, so a sample may differ in the last place where
-// the two libraries round differently (tests/test_gpu_parity.py measures how often).
+// domain-specific log / sqrt / sincos of channel_math.hpp instead of glibc's, so a sample may differ
+// in the last place where the two round differently (tests/test_gpu_parity.py bounds how often).
 // Compiled with -ffp-contract=off: x + scaling * g and dx*dx + dy*dy must not fuse.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -23,6 +23,11 @@
 #include "acs_persist.hpp"
 #include "acs_reg.hpp"
 #include "trellis.hpp"
+
+#define CCV_HD __device__
+__device__ __forceinline__ double ccv_rcp_approx(double d) { return __builtin_amdgcn_rcp(d); }
+__device__ __forceinline__ double ccv_rsq_approx(double x) { return __builtin_amdgcn_rsq(x); }
+#include "channel_math.hpp"
 
 namespace ccv {
 
@@ -261,10 +266,11 @@ struct ChannelSource {
         u1 = div_rand_max(rng.next());
         u2 = div_rand_max(rng.next());
       } while (u1 == 0.0);
-      const double R = sqrt(-2.0 * log(u1));
-      const double Tt = 2.0 * 3.14159265358979323846 * u2;   // 2.0 * M_PI * u2
+      // R = sqrt(-2 ln u1), (sin, cos)(2 pi u2): channel_math.hpp (a few ulp in double; 2e-8 or fewer
+      // of the fp32 samples differ from glibc's, 268 M host draws, profiles/r04_chanmath_check.txt)
+      const double R = chanmath::sqrt_nonneg(chanmath::neg2_log(u1));
       double sn, cs;
-      sincos(Tt, &sn, &cs);
+      chanmath::sincos_2pi(u2, &sn, &cs);
       x = (float)((double)x + (double)scaling * (R * cs));
       y = (float)((double)y + (double)scaling * (R * sn));
       if (hard_demap) {   // common/hard-demapper.c:66-80: snap to the first nearest point
