@@ -27,6 +27,14 @@
 #define CCV_HD __device__
 __device__ __forceinline__ double ccv_rcp_approx(double d) { return __builtin_amdgcn_rcp(d); }
 __device__ __forceinline__ double ccv_rsq_approx(double x) { return __builtin_amdgcn_rsq(x); }
+// a * b + c with a loop-invariant c: the three-address v_fma_f64 (the compiler otherwise picks the
+// two-address v_fmac_f64 and copies the hoisted constant into the accumulator first, one v_mov_b64
+// per Horner step)
+__device__ __forceinline__ double ccv_fma_const(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 #include "channel_math.hpp"
 
 namespace ccv {
@@ -256,10 +264,19 @@ struct ChannelSource {
       static_assert(C.n >= 1 && C.n <= 3, "the reference has constellations for n = 1..3");
       constexpr const float* pts = Constellation<C.n>::pts;
       float x = 0.f, y = 0.f;
+      if constexpr (C.n <= 2) {
+        // n = 1, 2: the points are (+-a, +-a), the signs the symbol's bits (n = 2: x <- bit 1,
+        // y <- bit 0; n = 1: both <- bit 0) -- two sign flips instead of a compare-select chain
+        static_assert(pts[0] == pts[1] && (C.n == 1 ? pts[2] == -pts[0] : pts[4] == -pts[0] && pts[3] == -pts[1]));
+        const uint32_t a = __builtin_bit_cast(uint32_t, pts[0]);
+        x = __builtin_bit_cast(float, a ^ (((sym >> (C.n - 1)) & 1u) << 31));
+        y = __builtin_bit_cast(float, a ^ ((sym & 1u) << 31));
+      } else {
 #pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        x = sym == (uint32_t)k ? pts[2 * k] : x;
-        y = sym == (uint32_t)k ? pts[2 * k + 1] : y;
+        for (int k = 0; k < NS; ++k) {
+          x = sym == (uint32_t)k ? pts[2 * k] : x;
+          y = sym == (uint32_t)k ? pts[2 * k + 1] : y;
+        }
       }
       double u1, u2;
       do {

@@ -19,9 +19,10 @@
 // match rate over 2^28 draws on the host with a reduced-precision rcp / rsq, profiles/
 // r04_chanmath_check.txt; the device tests hold it to >= 99.9 %, test_device_channel_awgn).
 //
-// The includer defines CCV_HD (function qualifiers) and ccv_rcp_approx / ccv_rsq_approx (device:
+// The includer defines CCV_HD (function qualifiers), ccv_rcp_approx / ccv_rsq_approx (device:
 // the v_rcp_f64 / v_rsq_f64 hardware approximations; the host checker: emulations with the low 28
-// mantissa bits cleared, so the Newton / Goldschmidt steps are exercised as on the device).
+// mantissa bits cleared, so the Newton / Goldschmidt steps are exercised as on the device) and
+// ccv_fma_const (a * b + c, c a constant: the device forces the three-address FMA).
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -59,15 +60,15 @@ CCV_HD inline double neg2_log(double u) {
   const double z = s * s;
   // 2 atanh(s) = 2s + s z (2/3 + 2/5 z + ... + 2/21 z^9)
   double p = 2.0 / 21.0;
-  p = __builtin_fma(p, z, 2.0 / 19.0);
-  p = __builtin_fma(p, z, 2.0 / 17.0);
-  p = __builtin_fma(p, z, 2.0 / 15.0);
-  p = __builtin_fma(p, z, 2.0 / 13.0);
-  p = __builtin_fma(p, z, 2.0 / 11.0);
-  p = __builtin_fma(p, z, 2.0 / 9.0);
-  p = __builtin_fma(p, z, 2.0 / 7.0);
-  p = __builtin_fma(p, z, 2.0 / 5.0);
-  p = __builtin_fma(p, z, 2.0 / 3.0);
+  p = ccv_fma_const(p, z, 2.0 / 19.0);
+  p = ccv_fma_const(p, z, 2.0 / 17.0);
+  p = ccv_fma_const(p, z, 2.0 / 15.0);
+  p = ccv_fma_const(p, z, 2.0 / 13.0);
+  p = ccv_fma_const(p, z, 2.0 / 11.0);
+  p = ccv_fma_const(p, z, 2.0 / 9.0);
+  p = ccv_fma_const(p, z, 2.0 / 7.0);
+  p = ccv_fma_const(p, z, 2.0 / 5.0);
+  p = ccv_fma_const(p, z, 2.0 / 3.0);
   const double lnm = __builtin_fma(s * z, p, 2.0 * s);
   // ln 2 split so that e * LN2_HI is exact for |e| < 2^11
   constexpr double LN2_HI = 6.93147180369123816490e-01;   // 0x3FE62E42FEE00000
@@ -98,21 +99,21 @@ CCV_HD inline void sincos_2pi(double u, double* sn, double* cs) {
   const double z = r * r;
   // sin r = r + r z S(z), S to the r^15 term; cos r = 1 + z C(z), C to the r^16 term
   double ps = -1.0 / 1307674368000.0;
-  ps = __builtin_fma(ps, z, 1.0 / 6227020800.0);
-  ps = __builtin_fma(ps, z, -1.0 / 39916800.0);
-  ps = __builtin_fma(ps, z, 1.0 / 362880.0);
-  ps = __builtin_fma(ps, z, -1.0 / 5040.0);
-  ps = __builtin_fma(ps, z, 1.0 / 120.0);
-  ps = __builtin_fma(ps, z, -1.0 / 6.0);
+  ps = ccv_fma_const(ps, z, 1.0 / 6227020800.0);
+  ps = ccv_fma_const(ps, z, -1.0 / 39916800.0);
+  ps = ccv_fma_const(ps, z, 1.0 / 362880.0);
+  ps = ccv_fma_const(ps, z, -1.0 / 5040.0);
+  ps = ccv_fma_const(ps, z, 1.0 / 120.0);
+  ps = ccv_fma_const(ps, z, -1.0 / 6.0);
   const double sr = __builtin_fma(r * z, ps, r);
   double pc = 1.0 / 20922789888000.0;
-  pc = __builtin_fma(pc, z, -1.0 / 87178291200.0);
-  pc = __builtin_fma(pc, z, 1.0 / 479001600.0);
-  pc = __builtin_fma(pc, z, -1.0 / 3628800.0);
-  pc = __builtin_fma(pc, z, 1.0 / 40320.0);
-  pc = __builtin_fma(pc, z, -1.0 / 720.0);
-  pc = __builtin_fma(pc, z, 1.0 / 24.0);
-  pc = __builtin_fma(pc, z, -0.5);
+  pc = ccv_fma_const(pc, z, -1.0 / 87178291200.0);
+  pc = ccv_fma_const(pc, z, 1.0 / 479001600.0);
+  pc = ccv_fma_const(pc, z, -1.0 / 3628800.0);
+  pc = ccv_fma_const(pc, z, 1.0 / 40320.0);
+  pc = ccv_fma_const(pc, z, -1.0 / 720.0);
+  pc = ccv_fma_const(pc, z, 1.0 / 24.0);
+  pc = ccv_fma_const(pc, z, -0.5);
   const double cr = __builtin_fma(z, pc, 1.0);
   // 2 pi u = q pi/2 + r
   const int qi = (int)q & 3;

@@ -23,6 +23,7 @@ static double trunc28(double x) {
 }
 static double ccv_rcp_approx(double d) { return trunc28(1.0 / d); }
 static double ccv_rsq_approx(double x) { return x > 0 ? trunc28(1.0 / std::sqrt(x)) : INFINITY; }
+static double ccv_fma_const(double a, double b, double c) { return __builtin_fma(a, b, c); }
 #define CCV_HD
 #include "../convolutional-codes_amd/csrc/channel_math.hpp"
 
