@@ -1,6 +1,6 @@
 # Round 4: (1) Fano on the BSC -- received rows in LDS (default) or prefetched from global memory,
 # expected-symbol table on / off, bench.py round-robin; (2) the K = 9 sweep's two kernels at 12 dB and
-# 14 dB, one rocprof kernel trace per point (why 12 dB runs slower).
+# 14 dB, one rocprof kernel trace per point (why 12 dB runs slower); (3) PMC passes.
 set -u
 export PYTHONPATH=$PWD/convolutional-codes_amd TMPDIR=/tmp
 O=gpurun_out/r04n
@@ -24,4 +24,10 @@ import csv
 for r in csv.reader(open('$O/prof_$pt/run_kernel_stats.csv')):
     print('$pt dB', r[0][:40], r[1:4])"
 done
+# (3) PMC passes (FETCH / WRITE / SQ / STALL) for the bench lines that have none yet
+bash tools/pmc_workload.sh --code k7:true > $O/pmc_k7true.log 2>&1 || { tail -5 $O/pmc_k7true.log; exit 1; }
+bash tools/pmc_workload.sh --code k9:true --frames 32 > $O/pmc_k9true.log 2>&1 || { tail -5 $O/pmc_k9true.log; exit 1; }
+bash tools/pmc_workload.sh --decoder fano --reps 1 > $O/pmc_fano.log 2>&1 || { tail -5 $O/pmc_fano.log; exit 1; }
+bash tools/pmc_workload.sh > $O/pmc_k7.log 2>&1 || { tail -5 $O/pmc_k7.log; exit 1; }
+cp gpurun_out/pmc/pmc_workloads.json $O/pmc_workloads_new.json
 echo done
