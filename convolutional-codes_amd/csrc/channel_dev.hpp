@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "acs_multi.hpp"
 #include "acs_persist.hpp"
@@ -139,7 +140,7 @@ struct Encoder {
   uint32_t state;
   int t;
   __device__ __forceinline__ uint32_t symbol_and_advance(int blen) {
-    const uint32_t i = t < blen ? (w[0] >> 31) : 0u;
+    const uint32_t i = bit(blen);
     const uint64_t sr = ((uint64_t)state << (64 - C.K)) | ((uint64_t)i << 63);
     uint32_t e = 0;
 #pragma unroll
@@ -150,15 +151,23 @@ struct Encoder {
       e = (e << 1) | p;
     }
     state = (state >> 1) | (i << (C.K - 2));
+    advance(blen);
+    return e;
+  }
+  // the next info bit (0 past blen) is the top bit of w[0]; the window moves by a word every 32
+  // steps behind a real (wave-uniform) branch: the empty volatile asm keeps the compiler from
+  // speculating the word shift into 7 selects on every step
+  __device__ __forceinline__ uint32_t bit(int blen) const { return t < blen ? (w[0] >> 31) : 0u; }
+  __device__ __forceinline__ void advance(int) {
     ++t;
     if ((t & 31) == 0) {
 #pragma unroll
       for (int k = 0; k < 7; ++k) w[k] = w[k + 1];
       w[7] = 0;
+      asm volatile("");
     } else {
       w[0] <<= 1;
     }
-    return e;
   }
 };
 
@@ -174,7 +183,7 @@ struct EncoderRT {
   int K, gen;
   uint64_t poly[NP];
   __device__ __forceinline__ uint32_t symbol_and_advance(int blen) {
-    const uint64_t i = t < blen ? (w[0] >> 31) : 0u;
+    const uint64_t i = bit(blen);
     const uint64_t sr = (K < 64 ? state << (64 - K) : state) | (i << 63);
     uint32_t e = 0;
 #pragma unroll
@@ -185,15 +194,23 @@ struct EncoderRT {
       e = (e << 1) | p;
     }
     state = (state >> 1) | (i << (K - 2));
+    advance(blen);
+    return e;
+  }
+  // the next info bit (0 past blen) is the top bit of w[0]; the window moves by a word every 32
+  // steps behind a real (wave-uniform) branch: the empty volatile asm keeps the compiler from
+  // speculating the word shift into 7 selects on every step
+  __device__ __forceinline__ uint32_t bit(int blen) const { return t < blen ? (w[0] >> 31) : 0u; }
+  __device__ __forceinline__ void advance(int) {
     ++t;
     if ((t & 31) == 0) {
 #pragma unroll
       for (int k = 0; k < 7; ++k) w[k] = w[k + 1];
       w[7] = 0;
+      asm volatile("");
     } else {
       w[0] <<= 1;
     }
-    return e;
   }
 };
 
@@ -307,11 +324,13 @@ struct ChannelSource {
       }
       constexpr float ndx = pts[0] - pts[2], ndy = pts[1] - pts[3];
       constexpr float nd = (ndx * ndx) + (ndy * ndy);
-#pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        const float dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
-        BM[k] = div_const<nd>((dx * dx) + (dy * dy));
-      }
+      // the points as compile-time constants (a loop over pts[] reads them from memory), so the
+      // coordinates the points share give one subtraction and one square each
+      [&]<int... k>(std::integer_sequence<int, k...>) __attribute__((always_inline)) {
+        ((BM[k] = div_const<nd>(((x - Constellation<C.n>::pts[2 * k]) * (x - Constellation<C.n>::pts[2 * k])) +
+                                ((y - Constellation<C.n>::pts[2 * k + 1]) * (y - Constellation<C.n>::pts[2 * k + 1])))),
+         ...);
+      }(std::make_integer_sequence<int, NS>{});
       if (out && t < T) {
         float* o = reinterpret_cast<float*>(out) + (size_t)t * NS;
 #pragma unroll
