@@ -120,6 +120,50 @@ __device__ __forceinline__ void multi2_growth(float (&M)[X::NR], const float (&B
   }
 }
 
+// The cross phase through ds_swizzle (XSWZ; acs_multi.hpp multi_cross_swz): any DPP / permlane /
+// readlane VALU instruction drops the wave's whole VALU stream to about half rate for ~800
+// instructions on gfx950, and the cross phase issues 256 of them per period, so the
+// even / odd predecessors come from the pair's lanes through the LDS crossbar instead -- registers in
+// chunks of G, the swizzles of chunk c + 1 issued before the ACS of chunk c.
+template <CodeSpec C, int P, class X, int G = 8>
+__device__ __forceinline__ void multi2_cross_swz(float (&M)[X::NR], const float (&BM)[4], bool qb,
+                                                 uint32_t (&D)[4]) {
+  static_assert(X::is_lane(P), "cross-lane phase");
+  constexpr int NR = X::NR;
+  constexpr int NC = NR / G;
+  static_assert(NR % G == 0, "whole chunks");
+  float E[2][G], O[2][G];
+  auto issue = [&]<int c>() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int R = NR - 1 - (c * G + i);
+      E[c & 1][i] = swz_quad<0, 0, 2, 2>(M[R]);
+      O[c & 1][i] = swz_quad<1, 1, 3, 3>(M[R]);
+    }
+  };
+  auto compute = [&]<int c>() __attribute__((always_inline)) {
+    [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
+      ([&]() __attribute__((always_inline)) {
+        constexpr int R = NR - 1 - (c * G + is);
+        constexpr auto e = [](int q, int odd) { return expected_symbol(C, X::logical(0, R, P) | (uint32_t)odd, q); };
+        const float a0 = E[c & 1][is] + select_bm<2, e(0, 0), e(1, 0), 0, 0>(BM, qb, false);
+        const float a1 = O[c & 1][is] + select_bm<2, e(0, 1), e(1, 1), 0, 0>(BM, qb, false);
+        M[R] = vmin(a0, a1);
+        D[R >> 5] = shift_in(D[R >> 5], a0, a1);
+      }(), ...);
+    }(std::make_integer_sequence<int, G>{});
+  };
+  issue.template operator()<0>();
+  [&]<int... cs>(std::integer_sequence<int, cs...>) __attribute__((always_inline)) {
+    ([&]() __attribute__((always_inline)) {
+      if constexpr (cs + 1 < NC) issue.template operator()<cs + 1>();
+      __builtin_amdgcn_sched_barrier(0);
+      compute.template operator()<cs>();
+      __builtin_amdgcn_sched_barrier(0);
+    }(), ...);
+  }(std::make_integer_sequence<int, NC>{});
+}
+
 // Registers per scheduling group: a scheduling barrier after every kMulti2Group registers keeps the
 // compiler from hoisting the adds of many butterflies ahead of their mins (with 128 independent
 // butterflies per step it otherwise keeps old and new metrics alive together: 256 VGPRs + spills).
@@ -150,7 +194,7 @@ constexpr size_t multi2_slot_bytes() {
 #ifndef CCV_MULTI2_WAVES
 #define CCV_MULTI2_WAVES 2
 #endif
-template <CodeSpec C, int BLEN, int LB = 7>
+template <CodeSpec C, int BLEN, bool XSWZ = false, int LB = 7>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(CCV_MULTI2_WAVES)))
 void viterbi_multi2_slot(RegArgs a, int ngroups) {
   using X = Multi2<C, LB>;
@@ -237,7 +281,8 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
           multi2_growth_impl<C, P, X>(M, BM, qb, std::make_index_sequence<NR>{});
         } else {
           uint32_t D[4] = {0u, 0u, 0u, 0u};
-          multi2_step_impl<C, P, X>(M, BM, qb, D, std::make_index_sequence<NR>{});
+          if constexpr (XSWZ && X::is_lane(P)) multi2_cross_swz<C, P, X>(M, BM, qb, D);
+          else multi2_step_impl<C, P, X>(M, BM, qb, D, std::make_index_sequence<NR>{});
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{D[0], D[1], D[2], D[3]}, slot, col,
                                                  ((p - 1) * n + P) * STEPB, 0);
         }

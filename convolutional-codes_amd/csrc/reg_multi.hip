@@ -103,7 +103,9 @@ hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
     // frames); A/B forms: CCV_K9_SLOT_XSWZ=0 the same kernel with DPP adds (27.9; 4 waves per SIMD
     // with CCV_K9_SLOT_WAVES=4: 27.7), CCV_K9_TRUE_LANES=2 two lanes per block with DPP (27.5)
     if (!k9_true_four_lanes())
-      return launch_persistent(viterbi_multi2_slot<kMultiCodes[I], kPersistBlen>, a, ngroups, stream);
+      return k9_slot_xswz()
+                 ? launch_persistent(viterbi_multi2_slot<kMultiCodes[I], kPersistBlen, true>, a, ngroups, stream)
+                 : launch_persistent(viterbi_multi2_slot<kMultiCodes[I], kPersistBlen, false>, a, ngroups, stream);
     else if (k9_slot_xswz())
       return launch_persistent(viterbi_multi_slot<kMultiCodes[I], kPersistBlen, 3, true>, a, ngroups, stream);
     else if (k9_slot_waves() == 4)
