@@ -125,7 +125,10 @@ __device__ __forceinline__ void multi2_growth(float (&M)[X::NR], const float (&B
 // instructions on gfx950, and the cross phase issues 256 of them per period, so the
 // even / odd predecessors come from the pair's lanes through the LDS crossbar instead -- registers in
 // chunks of G, the swizzles of chunk c + 1 issued before the ACS of chunk c.
-template <CodeSpec C, int P, class X, int G = 8>
+#ifndef CCV_MULTI2_XG
+#define CCV_MULTI2_XG 8
+#endif
+template <CodeSpec C, int P, class X, int G = CCV_MULTI2_XG>
 __device__ __forceinline__ void multi2_cross_swz(float (&M)[X::NR], const float (&BM)[4], bool qb,
                                                  uint32_t (&D)[4]) {
   static_assert(X::is_lane(P), "cross-lane phase");

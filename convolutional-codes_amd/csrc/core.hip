@@ -466,7 +466,12 @@ const char* ccv_plan_kernel_variant(const ccv_plan* p) {
   if (p->stack) return "stack";
   if (p->fano) return "fano";
   if (!register_path(*p)) return "generic";
-  if (wide_kernel(*p, false)) return p->d.gen_mode == CCV_GEN_REF_X86 ? "persistent-wide" : "persistent-slot";
+  if (wide_kernel(*p, false)) {
+    if (p->d.gen_mode == CCV_GEN_REF_X86) return "persistent-wide";
+    // the slot kernel's groups: 32 blocks (two lanes per block) or 16 (four lanes)
+    return ccv::multi_wide_group_blocks(p->multi_index) == ccv::kRegThreads / 2 ? "persistent-slot2"
+                                                                                 : "persistent-slot4";
+  }
   if (persist_kernel(*p, false)) return "persistent";
   if (p->multi_index >= 0) return regdec_kernel(*p, false) ? "multilane-regdec" : "multilane";
   return regdec_kernel(*p, false) ? "register-regdec" : "register";

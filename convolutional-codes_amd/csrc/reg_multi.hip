@@ -52,11 +52,11 @@ constexpr std::array<RegLaunchFn, sizeof...(I)> make_persist(std::index_sequence
   return {((kMultiCodes[I].K == 9 && kMultiCodes[I].n == 2) ? &launch_persist<I> : nullptr)...};
 }
 
-// The true-parity K = 9 slot kernel: four lanes per block (default) or two (CCV_K9_TRUE_LANES=2, A/B)
+// The true-parity K = 9 slot kernel: two lanes per block (default) or four (CCV_K9_TRUE_LANES=4, A/B)
 inline bool k9_true_four_lanes() {
   static const bool four = [] {
     const char* env = std::getenv("CCV_K9_TRUE_LANES");
-    return env == nullptr || env[0] != '2';
+    return env != nullptr && env[0] == '4';
   }();
   return four;
 }
@@ -71,7 +71,7 @@ inline int k9_slot_waves() {
   return w;
 }
 
-// the four-lane slot kernel's cross-lane phases through ds_swizzle (default) or DPP (CCV_K9_SLOT_XSWZ=0)
+// the slot kernels' cross-lane phases through ds_swizzle (default) or DPP (CCV_K9_SLOT_XSWZ=0)
 inline bool k9_slot_xswz() {
   static const bool v = [] {
     const char* env = std::getenv("CCV_K9_SLOT_XSWZ");
@@ -94,14 +94,12 @@ hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
     // bit-identical (tools/k9_bench.hip, profiles/r03_k9_wide*.txt)
     return launch_persistent(viterbi_wide_persist<kMultiCodes[I], kPersistBlen, 0, 2>, a, ngroups, stream);
   else if constexpr (has_slot_kernel<I>())
-    // true parity (256 distinct metrics): four lanes per block, the main periods as a loop with the
-    // decisions through a per-wave slot, so the code fits the instruction cache (acs_multi.hpp
-    // viterbi_multi_slot)
-    // two lanes per block (acs_multi2.hpp); CCV_K9_TRUE_LANES=4: four lanes (acs_multi.hpp
-    // viterbi_multi_slot: 134 VGPRs, 3 waves per SIMD; a 4-wave build spills 15 VGPRs to scratch)
-    // four lanes per block, cross-lane phases through ds_swizzle (production: 34.1 Gbit/s at 32
-    // frames); A/B forms: CCV_K9_SLOT_XSWZ=0 the same kernel with DPP adds (27.9; 4 waves per SIMD
-    // with CCV_K9_SLOT_WAVES=4: 27.7), CCV_K9_TRUE_LANES=2 two lanes per block with DPP (27.5)
+    // true parity (256 distinct metrics), the main periods as a loop with the decisions through a
+    // per-wave slot. Production: two lanes per block (acs_multi2.hpp, 128 metrics per lane), the
+    // cross phase through ds_swizzle: 34.5-34.9 Gbit/s at 32 frames against 33.3-33.6 for four lanes
+    // with ds_swizzle (acs_multi.hpp viterbi_multi_slot, CCV_K9_TRUE_LANES=4) on one box
+    // (profiles/r04r/). A/B forms: CCV_K9_SLOT_XSWZ=0 the DPP cross phases (two lanes 27.5, four
+    // 27.9), CCV_K9_SLOT_WAVES=4 the 4-waves-per-SIMD four-lane build (27.7).
     if (!k9_true_four_lanes())
       return k9_slot_xswz()
                  ? launch_persistent(viterbi_multi2_slot<kMultiCodes[I], kPersistBlen, true>, a, ngroups, stream)

@@ -90,8 +90,9 @@ int ccv_plan_trellis(const ccv_plan* plan, uint8_t* exp);
 int ccv_plan_decision_storage(const ccv_plan* plan);
 
 /* Name of the kernel a ccv_decode_device call without decision export runs: "persistent",
- * "persistent-wide" (K = 9, one lane per block), "register-regdec", "register", "multilane-regdec",
- * "multilane", "generic", "stack" or "fano". */
+ * "persistent-wide" (K = 9, one lane per block), "persistent-slot2" / "persistent-slot4" (K = 9 true
+ * parity, two / four lanes per block), "register-regdec", "register", "multilane-regdec", "multilane",
+ * "generic", "stack" or "fano". */
 const char* ccv_plan_kernel_variant(const ccv_plan* plan);
 
 /* Grid (resident waves = occupancy x CUs, whole SIMDs) of the plan's persistent kernel: the value

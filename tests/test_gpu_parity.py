@@ -436,7 +436,7 @@ def test_k9_wide_kernel(torch_cuda, nb, gen):
     torch = torch_cuda
     c = K9.with_(gen_mode=gen)
     plan = Plan(c, SOFT)
-    assert plan.variant == ("persistent-wide" if gen == GEN_REF_X86 else "persistent-slot")
+    assert plan.variant == ("persistent-wide" if gen == GEN_REF_X86 else "persistent-slot2")
     assert plan.decisions == "slot"
     info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(3.0), 4242 + nb)
     d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
