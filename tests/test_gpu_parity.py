@@ -428,8 +428,8 @@ def test_multilane_shapes(K, nb, blen):
 @pytest.mark.parametrize("nb", [1, 15, 16, 17, 63, 64, 65, 3 * 64 + 5, 150000])
 def test_k9_wide_kernel(torch_cuda, nb, gen):
     """K = 9 soft at blen 40 runs a persistent kernel whose decisions go through a per-wave scratch
-    slot: one lane per block for the x86-idiom code (acs_wide.hpp), four lanes per block with the main
-    periods as a loop for the true-parity code (acs_multi.hpp viterbi_multi_slot). Ragged batches and
+    slot: one lane per block for the x86-idiom code (acs_wide.hpp), two lanes per block with the main
+    periods as a loop for the true-parity code (acs_multi2.hpp viterbi_multi2_slot). Ragged batches and
     more groups than resident waves (150,000 blocks: each wave decodes several groups through its one
     slot) decode exactly as the non-persistent four-lane kernel (FLAG_NO_PERSISTENT) and, on a
     sample, the oracle; the fused error count equals the host count."""
@@ -450,6 +450,40 @@ def test_k9_wide_kernel(torch_cuda, nb, gen):
     assert np.array_equal(out, four_lane.decode_host(rx))
     sample = np.unique(np.linspace(0, nb - 1, min(nb, 300)).astype(np.int64))
     assert np.array_equal(out[sample], O.viterbi_soft(_ocode(c), rx[sample]))
+
+
+_LANES_SCRIPT = r'''
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from ccviterbi import K9, SOFT, GEN_TRUE_PARITY, Plan, channel as ch
+c = K9.with_(gen_mode=GEN_TRUE_PARITY)
+nb = int(sys.argv[2])
+_, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 515)
+plan = Plan(c, SOFT)
+print(plan.variant)
+np.save(sys.argv[3], plan.decode_host(rx))
+'''
+
+
+@pytest.mark.parametrize("lanes,variant", [("4", "persistent-slot4"), ("2", "persistent-slot2")])
+def test_k9_true_lane_variants(torch_cuda, tmp_path, lanes, variant):
+    """The true-parity K = 9 kernel's A/B forms (CCV_K9_TRUE_LANES, read once per process, so each
+    runs in a child process): four lanes per block (acs_multi.hpp) and two (acs_multi2.hpp, the
+    default) decode a ragged multi-group batch identically to the oracle."""
+    import os
+    import subprocess
+    import sys
+    from conftest import REPO
+    nb = 3 * 2048 + 77
+    out_path = str(tmp_path / "out.npy")
+    env = dict(os.environ, CCV_K9_TRUE_LANES=lanes)
+    r = subprocess.run([sys.executable, "-c", _LANES_SCRIPT, os.path.join(REPO, "convolutional-codes_amd"),
+                        str(nb), out_path], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[-1] == variant
+    c = K9.with_(gen_mode=GEN_TRUE_PARITY)
+    _, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 515)
+    assert np.array_equal(np.load(out_path), O.viterbi_soft(_ocode(c), rx))
 
 
 def test_multilane_error_count_and_no_decision_export(torch_cuda):
