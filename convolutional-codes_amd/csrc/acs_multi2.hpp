@@ -167,6 +167,45 @@ __device__ __forceinline__ void multi2_cross_swz(float (&M)[X::NR], const float 
   }(std::make_integer_sequence<int, NC>{});
 }
 
+// Growth cross phase through ds_swizzle (XSWZ): every new state is its even predecessor (the pair's
+// lane 0, same register) plus the branch metric, in chunks of G registers.
+template <CodeSpec C, int P, class X, int G = CCV_MULTI2_XG>
+__device__ __forceinline__ void multi2_growth_cross_swz(float (&M)[X::NR], const float (&BM)[4], bool qb) {
+  static_assert(X::is_lane(P), "cross-lane phase");
+  constexpr int NR = X::NR;
+  auto chunk = [&]<int c>() __attribute__((always_inline)) {
+    float E[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) E[i] = swz_quad<0, 0, 2, 2>(M[c * G + i]);
+    [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
+      ([&]() __attribute__((always_inline)) {
+        constexpr int R = c * G + is;
+        constexpr auto e = [](int q) { return expected_symbol(C, X::logical(0, R, P), q); };
+        M[R] = E[is] + select_bm<2, e(0), e(1), 0, 0>(BM, qb, false);
+      }(), ...);
+    }(std::make_integer_sequence<int, G>{});
+  };
+  [&]<int... cs>(std::integer_sequence<int, cs...>) __attribute__((always_inline)) {
+    (chunk.template operator()<cs>(), ...);
+  }(std::make_integer_sequence<int, NR / G>{});
+}
+
+// the pair's other lane (quad_perm [1,0,3,2]) -- ds_swizzle with XSWZ, DPP otherwise (the argmin and
+// the traceback; CCV_MULTI2_MISC_DPP=1 keeps DPP there for A/B)
+#ifndef CCV_MULTI2_MISC_DPP
+#define CCV_MULTI2_MISC_DPP 0
+#endif
+template <bool XSWZ>
+__device__ __forceinline__ uint32_t pair_swap_u32(uint32_t x) {
+  if constexpr (XSWZ && !CCV_MULTI2_MISC_DPP) return swz_quad_u32<1, 0, 3, 2>(x);
+  else return dpp_u32<0xB1>(x);
+}
+template <bool XSWZ>
+__device__ __forceinline__ float pair_swap(float x) {
+  if constexpr (XSWZ && !CCV_MULTI2_MISC_DPP) return swz_quad<1, 0, 3, 2>(x);
+  else return dpp<0xB1, float>(x);
+}
+
 // Registers per scheduling group: a scheduling barrier after every kMulti2Group registers keeps the
 // compiler from hoisting the adds of many butterflies ahead of their mins (with 128 independent
 // butterflies per step it otherwise keeps old and new metrics alive together: 256 VGPRs + spills).
@@ -281,7 +320,8 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
         const float BM[4] = {rowv.x, rowv.y, rowv.z, rowv.w};
         if constexpr (P + 1 < n) rowv = lds_read_b128<0>(rd + (swz ^ (uint32_t)((P + 1) * 16)));
         if constexpr (GROWTH) {
-          multi2_growth_impl<C, P, X>(M, BM, qb, std::make_index_sequence<NR>{});
+          if constexpr (XSWZ && !CCV_MULTI2_MISC_DPP && X::is_lane(P)) multi2_growth_cross_swz<C, P, X>(M, BM, qb);
+          else multi2_growth_impl<C, P, X>(M, BM, qb, std::make_index_sequence<NR>{});
         } else {
           uint32_t D[4] = {0u, 0u, 0u, 0u};
           if constexpr (XSWZ && X::is_lane(P)) multi2_cross_swz<C, P, X>(M, BM, qb, D);
@@ -305,7 +345,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     // lowest index
     static_assert(T % n == 0, "the persistent trellis ends on phase 0");
     float mn = tree_min<NR, float>(M);
-    mn = vmin(mn, dpp<0xB1, float>(mn));   // quad_perm [1,0,3,2]: the pair's minimum
+    mn = vmin(mn, pair_swap<XSWZ>(mn));   // the pair's minimum
     uint32_t ne[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -318,7 +358,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     const uint32_t r0 = eq_lo ? (uint32_t)__builtin_ctzll(eq_lo) : (eq_hi ? 64u + (uint32_t)__builtin_ctzll(eq_hi) : 0xFFu);
     uint32_t idx = r0 != 0xFFu ? multi2_phys<LB>((uint32_t)q, r0) : 0xFFFFFFFFu;
     {
-      const uint32_t o = dpp_u32<0xB1>(idx);
+      const uint32_t o = pair_swap_u32<XSWZ>(idx);
       idx = o < idx ? o : idx;
     }
     const uint32_t st = mn < __builtin_inff() ? idx : 0u;   // nothing below +inf: state 0
@@ -349,7 +389,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
           const uint32_t word = (pos & 64u) ? w23 : w01;
           const uint32_t own = (word >> (pos & 31u)) & 1u;
           uint32_t m = own << qself;
-          m |= dpp_u32<0xB1>(m);   // quad_perm [1,0,3,2]
+          m |= pair_swap_u32<XSWZ>(m);
           const uint32_t d = (m >> ql) & 1u;
           if constexpr (X::is_lane(P)) {
             ql = d;
