@@ -95,10 +95,10 @@ hipError_t launch_wide(const RegArgs& a, int ngroups, hipStream_t stream) {
     return launch_persistent(viterbi_wide_persist<kMultiCodes[I], kPersistBlen, 0, 2>, a, ngroups, stream);
   else if constexpr (has_slot_kernel<I>())
     // true parity (256 distinct metrics), the main periods as a loop with the decisions through a
-    // per-wave slot. Production: two lanes per block (acs_multi2.hpp, 128 metrics per lane), the
-    // cross phase through ds_swizzle: 34.5-34.9 Gbit/s at 32 frames against 33.3-33.6 for four lanes
-    // with ds_swizzle (acs_multi.hpp viterbi_multi_slot, CCV_K9_TRUE_LANES=4) on one box
-    // (profiles/r04r/). A/B forms: CCV_K9_SLOT_XSWZ=0 the DPP cross phases (two lanes 27.5, four
+    // per-wave slot. Production: two lanes per block (acs_multi2.hpp, 128 metrics per lane), every
+    // cross-lane move through ds_swizzle: 37.4-37.8 Gbit/s at 32 frames (profiles/r04t/) against
+    // 33.3-33.6 for four lanes with ds_swizzle (acs_multi.hpp viterbi_multi_slot, CCV_K9_TRUE_LANES=4,
+    // profiles/r04r/). A/B forms: CCV_K9_SLOT_XSWZ=0 the DPP cross phases (two lanes 27.5, four
     // 27.9), CCV_K9_SLOT_WAVES=4 the 4-waves-per-SIMD four-lane build (27.7).
     if (!k9_true_four_lanes())
       return k9_slot_xswz()
