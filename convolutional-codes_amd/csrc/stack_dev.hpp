@@ -403,7 +403,14 @@ __device__ __forceinline__ void row_min_min_u32_swz(uint32_t& a, uint32_t& b) {
 
 // LDS bytes per row: the block's symbols (16-byte aligned), 65 entry records (64 + a dummy), then
 // the 64 path metrics + the dummy (padded to 68)
+// CCV_STACK_SYMG=1 (A/B, soft input): the rows kernel reads the block's demapped symbols from global
+// memory (L2) instead of staging them in LDS -- 864 fewer LDS bytes per K = 15 search, so more
+// resident waves, against a cache round trip in the iteration's chain
+#ifndef CCV_STACK_SYMG
+#define CCV_STACK_SYMG 0
+#endif
 __host__ __device__ constexpr size_t stack_rows_sym_bytes(int T, int ns, bool hard) {
+  if (CCV_STACK_SYMG && !hard) return 0;
   return (((size_t)T * (size_t)ns * (hard ? 1 : 4)) + 15) & ~(size_t)15;
 }
 __host__ __device__ constexpr size_t stack_rows_row_bytes(int T, int ns, bool hard) {
@@ -480,12 +487,17 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
     return __shfl((int)b, rbase, 64);
   };
   // stage a block's symbols and the root entry; the row's LDS is private to its 16 lanes
+  constexpr bool kSymG = CCV_STACK_SYMG && !HARD;
+  const ET* gsyms = in;
   auto stage = [&](int b) {
     const ET* src = in + (size_t)b * per;
-    for (int i = l; i < per; i += kRowLanes) {
-      ET v = src[i];
-      if constexpr (HARD) v = (ET)(v & symmask);   // binary-symmetric-channel/stack-decoder.c:116-118
-      syms[i] = v;
+    gsyms = src;
+    if constexpr (!kSymG) {
+      for (int i = l; i < per; i += kRowLanes) {
+        ET v = src[i];
+        if constexpr (HARD) v = (ET)(v & symmask);   // binary-symmetric-channel/stack-decoder.c:116-118
+        syms[i] = v;
+      }
     }
     if (l == 0) ent[0] = make_uint4(esym_root << 8, 0u, 0u, 0u);
 #pragma unroll
@@ -566,6 +578,7 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       uint32_t es = symbols_of(est);
       ET r0, r1;
       if constexpr (HARD) { r0 = r1 = syms[ci]; }
+      else if constexpr (kSymG) { r0 = gsyms[ci * NS + e0]; r1 = gsyms[ci * NS + e1]; }
       else { r0 = syms[ci * NS + e0]; r1 = syms[ci * NS + e1]; }
       if (ext && c_next >= (uint32_t)tn) {
         // symbols at or beyond the frontier are still the previous block's (header of stack_decode)
