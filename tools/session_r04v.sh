@@ -1,5 +1,6 @@
 # Round 4: the true-parity sweeps (K = 9 (561,753) and K = 7 (171,133)) with the on-device channel at
-# 800 M bits per point, and a kernel trace of the K = 9 true-parity point (frames + two-lane decode).
+# 800 M bits per point, a kernel trace of the K = 9 true-parity point (frames + two-lane decode), and
+# the stack decoder's rate against its batch size.
 set -u
 export PYTHONPATH=$PWD/convolutional-codes_amd TMPDIR=/tmp
 O=gpurun_out/r04v
@@ -17,4 +18,13 @@ cd $GRAFT_REPO_ROOT && python3 -c "
 import csv
 for r in csv.reader(open('$O/prof/run_kernel_stats.csv')):
     print(r[0][:40], r[1:4])"
+# stack decoder: batch size vs rate (the persistent rows' tail: waves live ~72 % of the 4-frame launch)
+for f in 4 16 32; do
+  for ch in awgn bsc; do
+    timeout -k 10 300 python bench.py --decoder stack --channel $ch --frames $f --steps 5 --warmup 1 --no-cpu-baseline > $O/stack_${ch}_f$f.log 2>&1 || { echo "stack $f failed"; tail -3 $O/stack_${ch}_f$f.log; exit 1; }
+    python3 -c "
+import json; d=json.loads(open('$O/stack_${ch}_f$f.log').read().strip().splitlines()[-1])
+print('stack $ch frames $f', d['value'], d['kernel_ms'])"
+  done
+done
 echo done
