@@ -113,7 +113,10 @@ class DeviceChannelDecoder:
         self.torch = torch
         self.device = torch.device(device if device is not None else "cuda")
         if chunk_blocks is None:
-            chunk_blocks = frame_blocks * max(1, (2_600_000 if decoder == "viterbi" else 200_000) // frame_blocks)
+            # stack: 32 frames per launch, where the persistent rows' tail of long searches weighs
+            # little (568 Mbit/s at 4 frames, 863 at 32)
+            per_launch = {"viterbi": 2_600_000, "stack": 800_000}.get(decoder, 200_000)
+            chunk_blocks = frame_blocks * max(1, per_launch // frame_blocks)
         self.chunk = chunk_blocks
         # Viterbi: one plan generates and decodes (fused); stack / Fano: the sequential plan itself
         # generates the frames (CCV_CHANNEL_FRAMES_ONLY, no Viterbi plan, any K) and then decodes them

@@ -29,8 +29,8 @@ run code0_bsc 300 --code code0 --channel bsc                   # config 1 code a
 run k9 300 --code k9 --frames 32                               # config 3 (port + AVX2 baselines)
 run k7_true 300 --code k7:true                                 # textbook (171,133)
 run k9_true 300 --code k9:true --frames 32                     # textbook (561,753)
-run stack 300 --decoder stack --frames 4 --steps 5 --warmup 1  # config 5
-run stack_bsc 300 --decoder stack --channel bsc --frames 4 --steps 5 --warmup 1
+run stack 300 --decoder stack --frames 16 --steps 5 --warmup 1  # config 5 (16 frames: DESIGN 4.5)
+run stack_bsc 300 --decoder stack --channel bsc --frames 16 --steps 5 --warmup 1
 run fano 600 --decoder fano --steps 3 --warmup 1 --no-cpu-baseline
 run fano_bsc 600 --decoder fano --channel bsc --steps 3 --warmup 1 --no-cpu-baseline
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
