@@ -28,6 +28,8 @@ bool stack_symtab_eligible(int n, int K, int T);                         // stac
 hipError_t launch_stack_symtab(uint16_t* tab, const StackArgs& a, hipStream_t s);   // stack.hip
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s);     // stack.hip
 size_t fano_order_bytes(int nblocks);                                    // stack.hip
+hipError_t launch_noise_order(const void* in, int n, int T, int nblocks, void* scratch, size_t bytes,
+                              const uint32_t** order, hipStream_t s);    // stack.hip
 hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
                              hipStream_t s);                             // stack.hip
 }
@@ -842,6 +844,16 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
     if (ccv::stack_symtab_eligible(a.n, a.K, a.T)) {
       if (ensure_symtab(p, stream)) return -1;
       a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
+    }
+    // soft input: noisiest blocks first (the Fano decoder's order, stack.hip launch_noise_order), so
+    // the long searches do not form the launch's tail; CCV_STACK_ORDER=0: natural order
+    bool order = p->d.channel == CCV_SOFT && (a.n == 2 || a.n == 3) && nblocks > 64;
+    if (const char* env = std::getenv("CCV_STACK_ORDER")) order = order && env[0] != '0';
+    if (order) {
+      const size_t need = ccv::fano_order_bytes(a.nblocks);
+      if (p->order.grow(need, stream)) return -1;
+      HIP_TRY(ccv::launch_noise_order(a.in, a.n, a.T, a.nblocks, p->order.ptr, p->order.bytes, &a.order,
+                                      stream));
     }
   }
   HIP_TRY(ccv::launch_stack(a, p->d.channel == CCV_HARD, stream));

@@ -206,26 +206,31 @@ size_t fano_order_bytes(int nblocks) {
   return 16 * (size_t)nblocks + tmp + 256;
 }
 
-hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
-                             hipStream_t s) {
-  const size_t n = (size_t)a.nblocks;
+hipError_t launch_noise_order(const void* in_v, int n_out, int T, int nblocks, void* scratch, size_t bytes,
+                              const uint32_t** order, hipStream_t s) {
+  const size_t n = (size_t)nblocks;
   float* k_in = static_cast<float*>(scratch);
   float* k_out = k_in + n;
   uint32_t* i_in = reinterpret_cast<uint32_t*>(k_out + n);
   uint32_t* i_out = i_in + n;
   void* tmp = reinterpret_cast<void*>(((uintptr_t)(i_out + n) + 255) & ~(uintptr_t)255);
   size_t tmp_bytes = bytes - (size_t)(static_cast<char*>(tmp) - static_cast<char*>(scratch));
-  const float* in = static_cast<const float*>(a.in);
+  const float* in = static_cast<const float*>(in_v);
   const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  if (a.n == 2) hipLaunchKernelGGL((fano_score<4>), grid, block, 0, s, in, a.T, a.nblocks, k_in, i_in);
-  else if (a.n == 3) hipLaunchKernelGGL((fano_score<8>), grid, block, 0, s, in, a.T, a.nblocks, k_in, i_in);
+  if (n_out == 2) hipLaunchKernelGGL((fano_score<4>), grid, block, 0, s, in, T, nblocks, k_in, i_in);
+  else if (n_out == 3) hipLaunchKernelGGL((fano_score<8>), grid, block, 0, s, in, T, nblocks, k_in, i_in);
   else return hipErrorInvalidValue;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes, k_in, k_out, i_in, i_out, a.nblocks, 0,
+  e = hipcub::DeviceRadixSort::SortPairsDescending(tmp, tmp_bytes, k_in, k_out, i_in, i_out, nblocks, 0,
                                                    32, s);
   *order = i_out;
   return e;
+}
+
+hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
+                             hipStream_t s) {
+  return launch_noise_order(a.in, a.n, a.T, a.nblocks, scratch, bytes, order, s);
 }
 
 }  // namespace ccv
