@@ -845,10 +845,12 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
       if (ensure_symtab(p, stream)) return -1;
       a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
     }
-    // soft input: noisiest blocks first (the Fano decoder's order, stack.hip launch_noise_order), so
-    // the long searches do not form the launch's tail; CCV_STACK_ORDER=0: natural order
-    bool order = p->d.channel == CCV_SOFT && (a.n == 2 || a.n == 3) && nblocks > 64;
-    if (const char* env = std::getenv("CCV_STACK_ORDER")) order = order && env[0] != '0';
+    // CCV_STACK_ORDER=1 (A/B, soft input): noisiest blocks first, the Fano decoder's order
+    // (stack.hip launch_noise_order). Measured 3 % SLOWER than the natural order at 4 and 16 frames
+    // (profiles/r04x/), so off by default.
+    bool order = false;
+    if (const char* env = std::getenv("CCV_STACK_ORDER"))
+      order = env[0] == '1' && p->d.channel == CCV_SOFT && (a.n == 2 || a.n == 3) && nblocks > 64;
     if (order) {
       const size_t need = ccv::fano_order_bytes(a.nblocks);
       if (p->order.grow(need, stream)) return -1;
