@@ -887,6 +887,19 @@ def test_device_channel_ber_sweep_matches_host(torch_cuda):
                 assert abs(d.errors - h.errors) <= max(2, h.errors // 1000)
 
 
+@pytest.mark.parametrize("decoder,c,channel", [("viterbi", K7, SOFT), ("viterbi", K9, SOFT),
+                                               ("stack", CODEBOOK[0], HARD)], ids=["k7", "k9", "stack"])
+def test_device_channel_warm_up_changes_nothing(torch_cuda, decoder, c, channel):
+    """The sweep CLI's warm-up (DeviceChannelDecoder.warm_up: throw-away chunks from block 2^62 on)
+    leaves the counts of the points after it unchanged."""
+    point = 3.0 if channel == SOFT else 60000
+    fresh = sim.DeviceChannelDecoder(c, channel, 1000, 7, decoder=decoder, chunk_blocks=4000)
+    want = fresh(point, 5 << 40, 9000)
+    warm = sim.DeviceChannelDecoder(c, channel, 1000, 7, decoder=decoder, chunk_blocks=4000)
+    assert warm.warm_up(0.01) >= 1
+    assert warm(point, 5 << 40, 9000) == want
+
+
 @pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["ref", "true"])
 def test_device_channel_k9_frames_path_equals_fused(torch_cuda, gen):
     """K = 9 soft at blen 40: ccv_simulate_device writes the frames (channel_frames) and decodes them
