@@ -94,6 +94,8 @@ def core():
     L.ccv_fano_decode_device.restype = _i
     L.ccv_decode_host.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.ccv_decode_host.restype = _i
+    L.ccv_hbm_probe.argtypes = [_i, _vp, _vp, _sz, _vp, _vp]
+    L.ccv_hbm_probe.restype = _i
     L.ccv_device_count.argtypes = []
     L.ccv_device_count.restype = _i
     L.ccv_last_error.argtypes = []

@@ -163,58 +163,6 @@ constexpr bool twin_code() {
     return false;
 }
 
-// acs_step (soft, fp32) with the class layout, S <= 64: the 39 classes of K = 7 in 2 words.
-template <CodeSpec C>
-__device__ __forceinline__ uint64_t acs_step_twin(float (&M)[1 << (C.K - 1)], const float (&BM)[1 << C.n]) {
-  constexpr int S = 1 << (C.K - 1);
-  constexpr int H = S / 2;
-  using TT = TwinTable<C.K>;
-  static_assert(TT::words == 2, "two decision words per step");
-  float N[S];
-  uint32_t d[2] = {0u, 0u};
-  [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
-    ([&]() __attribute__((always_inline)) {
-      constexpr int j = H - 1 - js;
-      const float a0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 0)];
-      const float a1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 0)];
-      const float b0 = M[2 * j] + BM[expected_symbol(C, 2 * j, 1)];
-      const float b1 = M[2 * j + 1] + BM[expected_symbol(C, 2 * j + 1, 1)];
-      N[j] = vmin(a0, a1);
-      N[j + H] = vmin(b0, b1);
-      if constexpr (TT::rep[j] != 0) d[TT::pos[j] >> 5] = shift_in(d[TT::pos[j] >> 5], a0, a1);
-      if constexpr (TT::rep[j + H] != 0) d[TT::pos[j + H] >> 5] = shift_in(d[TT::pos[j + H] >> 5], b0, b1);
-    }(), ...);
-  }(std::make_integer_sequence<int, H>{});
-#pragma unroll
-  for (int s = 0; s < S; ++s) M[s] = N[s];
-  return ((uint64_t)d[1] << 32) | d[0];
-}
-
-// traceback_regs with the class layout: a state's decision bit comes from the LDS position table.
-template <int K, int F>
-__device__ __forceinline__ uint64_t traceback_twin(const uint64_t (&D)[F], uint32_t st, int F_rt,
-                                                   const uint8_t* pos) {
-  constexpr int S = 1 << (K - 1);
-  constexpr int T = F + K - 1;
-  static_assert(T <= 64, "history fits two words");
-  constexpr int SPLIT = 33 - K;
-  uint32_t h = st, hi = 0;
-#pragma unroll
-  for (int j = 0; j < F; ++j) {
-    const int m = F - 1 - j;
-    if (m % 8 == 7 || m == F - 1) {
-      if (m >= F_rt) continue;
-    }
-    const uint32_t d = (uint32_t)(D[m] >> pos[h & (S - 1)]);
-    h = (h << 1) | (d & 1u);
-    if (j + 1 == SPLIT) hi = h;
-  }
-  uint64_t H;
-  if constexpr (F <= SPLIT) H = h;
-  else H = ((uint64_t)hi << (F - SPLIT)) | (h & ((1u << (F - SPLIT)) - 1u));
-  return __builtin_bitreverse64(H);
-}
-
 // Output bytes (MSB-first, reference traceback :88) and the bit errors of the first blen bits
 // against the transmitted info bytes (consumer AWGN-channel/main.c:118-144). Static sizes: runtime
 // byte loops here cost the persistent kernels their register allocation (spills).
@@ -271,10 +219,12 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 }
 
 // Ablation switches for timing studies (tools/persist_bench.hip); production kernels use 0.
+// Measured and removed in round 5 (A/B recorded in DESIGN.md 4.1b / 4.1c): line-aligned DMA staging
+// (10 % less fetch, 17 % slower), one decision per value-numbering class (1.02x), staged loads +
+// ds_write instead of LDS-DMA (1.5 % slower).
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
-             kPersistDepth2 = 16, kPersistLineChunks = 32, kPersistNoMemRandom = 64,
-             kPersistNoDma = 128, kPersistNoLdsRead = 256, kPersistInputNt = 512, kPersistTwins = 1024,
-             kPersistStage = 2048 };
+             kPersistDepth2 = 16, kPersistNoMemRandom = 64, kPersistNoDma = 128, kPersistNoLdsRead = 256,
+             kPersistInputNt = 512 };
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -292,47 +242,13 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
   static_assert(BLEN >= 1 && BLEN <= kPersistMaxMain, "decisions of the main steps live in VGPRs");
   static_assert(NCH >= 4 && NCH % 2 == 0, "buffer = chunk parity across groups");
-  // Line-aligned staging (LINES, ablation kPersistLineChunks): block r of a group starts
-  // phi_r = r*T mod 8 steps into a 128-byte line, so its 8-step chunks straddle two lines and a line
-  // is fetched twice whenever the L2 dropped it between two chunks (PMC: 2.63 GB per launch for
-  // 1.91 GB of input; a line-aligned input (blen 42, T = 48) fetches 25 % less and keeps a higher
-  // clock). LINES instead has DMA k move block r's k-th ALIGNED line (steps 8k - phi_r ..; NCH + 1
-  // lines), two line buffers alternate, and window w reads each lane's steps from lines w and w + 1
-  // at lane-dependent slots. Bit-exact, 10 % less fetch (the line a block shares with the next is
-  // still fetched twice), but slower (persist_bench 0.345 vs 0.295 ms; profiles/r02_persist_bench.txt):
-  // not the production path.
-  constexpr bool LINES = (T % PF) != 0 && (ABLATE & kPersistLineChunks) != 0 && (ABLATE & kPersistNoMem) == 0;
-  constexpr bool DEPTH2 = !LINES && (ABLATE & kPersistDepth2) != 0;   // two chunks in flight
-  // STAGE: no LDS-DMA. A global_load_lds instruction holds the SIMD's VALU issue: 8 of them per 3,200
-  // butterfly instructions cost the stream 25 %, 16 cost 49 %, while 8 coalesced global_load_dwordx4
-  // into VGPRs cost nothing (tools/raterbench7.hip, profiles/r04c/raterbench7f.txt) -- and this kernel
-  // issues 8 per 8-step chunk (~1,600 VALU). So the chunk's 16-byte units (the DMA's unit mapping) are
-  // loaded into VGPRs at the chunk's first step, written to the other LDS buffer at its fifth (after
-  // vmcnt(0)) with ds_write_b128, and every step reads its row one step ahead. (Each lane loading its
-  // own block's rows instead -- 64 lines per instruction -- ran 0.61x: the address processing of the
-  // scattered loads stalls issue, round-4 A/B.)
-  constexpr bool STAGE = (ABLATE & kPersistStage) != 0 && !LINES && !DEPTH2 && (ABLATE & kPersistNoMem) == 0;
-  constexpr int NLINE = NCH + 1;              // aligned lines per block window sequence (LINES)
+  constexpr bool DEPTH2 = (ABLATE & kPersistDepth2) != 0;   // two chunks in flight
   using DW = DecWord<S>;
   const int lane = threadIdx.x;
   const int nb = a.nblocks;
   const int stride_groups = gridDim.x;
 
-  __shared__ __attribute__((aligned(1024))) unsigned char
-      lds[(LINES || DEPTH2 || STAGE) ? 2 * BUF : BUF];
-  // kPersistTwins (A/B, not the production path): one decision per value-numbering class of the
-  // x86-idiom K = 7 code (twins.hpp) -- 3.7 % fewer VALU, but the traceback's state -> (word, bit)
-  // lookup in LDS lengthens its dependent chain: 1.02x the time (profiles/r03_k7_twin_ab.txt)
-  constexpr bool TWINS = twin_code<C>() && (ABLATE & kPersistTwins) != 0 && S == 64;
-  __shared__ uint32_t twin_pos[TWINS ? S / 4 : 1];
-  if constexpr (TWINS) {
-    if (lane < S / 4) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v |= (uint32_t)TwinTable<C.K>::pos[4 * lane + k] << (8 * k);
-      twin_pos[lane] = v;
-    }
-  }
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[DEPTH2 ? 2 * BUF : BUF];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   constexpr uint32_t block_bytes = (uint32_t)T * 16;
   // DMA k of a chunk: lane l moves 16-byte unit j = l % 8 of block r = 8k + l / 8 of the group, from
@@ -344,42 +260,8 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   for (int k = 0; k < UPR; ++k) {
     const int r = k * (kRegThreads / UPR) + lane / UPR, j = lane % UPR;
     const int su = j ^ ((r / GRP) % UPR);
-    if constexpr (LINES) dma_off[k] = (((uint32_t)r * (uint32_t)T) >> 3) * 128 + (uint32_t)su * 16;
-    else dma_off[k] = (uint32_t)r * block_bytes + (uint32_t)su * 16;
+    dma_off[k] = (uint32_t)r * block_bytes + (uint32_t)su * 16;
   }
-  // LINES: the line DMA; groups holding the batch's last block clamp each unit into the buffer
-  const size_t total_bytes = (size_t)nb * block_bytes;
-  auto issue_line = [&](int g, int k, int buf) __attribute__((always_inline)) {
-    const size_t gbase = (size_t)g * kRegThreads * block_bytes;
-    if (g * kRegThreads + kRegThreads < nb) {
-      const unsigned char* base = in + gbase + k * 128;
-#pragma unroll
-      for (int kk = 0; kk < UPR; ++kk)
-        __builtin_amdgcn_global_load_lds(base + dma_off[kk], (lds_ptr_t)(lds + buf * BUF + kk * kRegThreads * 16),
-                                         16, 0, 0);
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < UPR; ++kk) {
-        size_t off = gbase + (size_t)k * 128 + dma_off[kk];
-        off = off + 16 <= total_bytes ? off : total_bytes - 16;
-        __builtin_amdgcn_global_load_lds(in + off, (lds_ptr_t)(lds + buf * BUF + kk * kRegThreads * 16), 16, 0, 0);
-      }
-    }
-  };
-  // LINES: byte offset (inside the two-buffer LDS block) of this lane's step x of a window, for
-  // window parity 0 (bit 13 = which buffer); odd windows flip bit 13
-  // (two 14-bit offsets per VGPR: 4 registers, where the K=7 true-parity build has none to spare)
-  uint32_t rd_pk[UPR / 2];
-  {
-    const int phi = (lane * T) & 7, sw = (lane / GRP) % UPR;
-#pragma unroll
-    for (int x = 0; x < UPR; x += 2) {
-      const uint32_t o0 = (uint32_t)(((x + phi) >> 3) * BUF + lane * ROWB + ((((x + phi) & 7) ^ sw) << 4));
-      const uint32_t o1 = (uint32_t)(((x + 1 + phi) >> 3) * BUF + lane * ROWB + ((((x + 1 + phi) & 7) ^ sw) << 4));
-      rd_pk[x / 2] = o0 | (o1 << 16);
-    }
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)lds;
   // Groups holding the batch's last block clamp every unit into the buffer (a lane past the batch
   // replays block nb-1; a unit past the block end re-reads its last step; neither is ever read).
   auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
@@ -410,58 +292,13 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   const uint32_t rd_base = (uint32_t)(uintptr_t)(lds_ptr_t)lds + (uint32_t)(lane * ROWB) +
                            (uint32_t)(((lane / GRP) % UPR) * 16);
 
-  // STAGE: the input as one buffer resource (byte offsets < 2^31: the host splits larger batches)
-  const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned char*>(in), 0,
-      (int)((size_t)nb * block_bytes < 0x7FFFFFFFu ? (size_t)nb * block_bytes : 0x7FFFFFFFu), 0x00020000);
-  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
-  u32x4s stg[UPR];
-  // chunk c of group gg into stg (unit k = the DMA's unit k); the group holding the batch's last
-  // block clamps each unit into the buffer, as issue_chunk does
-  auto load_chunk = [&](int gg, int c) __attribute__((always_inline)) {
-    if (gg * kRegThreads + kRegThreads < nb) {
-      const int soff = gg * kRegThreads * (int)block_bytes + c * PF * 16;
-#pragma unroll
-      for (int k = 0; k < UPR; ++k) stg[k] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, dma_off[k], soff, 0);
-    } else {
-#pragma unroll
-      for (int k = 0; k < UPR; ++k) {
-        const int r = k * (kRegThreads / UPR) + lane / UPR, j = lane % UPR;
-        const int su = j ^ ((r / GRP) % UPR);
-        const int gb = gg * kRegThreads + r < nb ? gg * kRegThreads + r : nb - 1;
-        uint32_t off = (uint32_t)(c * PF + su) * 16;
-        off = off < block_bytes ? off : block_bytes - 16;
-        stg[k] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, (uint32_t)gb * block_bytes + off, 0, 0);
-      }
-    }
-  };
-  auto store_chunk = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < UPR; ++k)
-      *reinterpret_cast<u32x4s*>(lds + buf * BUF + (k * kRegThreads + lane) * 16) = stg[k];
-    asm volatile("" ::: "memory");   // before any later LDS read (the reads are asm)
-  };
-
   uint32_t errors = 0;
   int g = blockIdx.x;
-  uint32_t gp = 0;   // LINES: buffer of the group's line 0 (flips per group: NLINE is odd)
-  if constexpr (STAGE) {
-    if (g < ngroups) {
-      load_chunk(g, 0);
-      wait_vmcnt<0>();
-      store_chunk(0);
-    }
+  if (!(ABLATE & kPersistNoMem) && g < ngroups) {
+    issue_chunk(g, 0, 0);
+    if constexpr (DEPTH2) issue_chunk(g, 1, 1);
   }
-  if (!(ABLATE & kPersistNoMem) && !STAGE && g < ngroups) {
-    if constexpr (LINES) {
-      issue_line(g, 0, 0);
-      issue_line(g, 1, 1);
-    } else {
-      issue_chunk(g, 0, 0);
-      if constexpr (DEPTH2) issue_chunk(g, 1, 1);
-    }
-  }
-  for (; g < ngroups; g += stride_groups, gp ^= (NLINE & 1)) {
+  for (; g < ngroups; g += stride_groups) {
     const int b = g * kRegThreads + lane;
     const bool has_next = g + stride_groups < ngroups;
     float M[S];
@@ -485,19 +322,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
                            __uint_as_float((r0 & 0x7FFFFFu) | 0x3F800000u), __uint_as_float((r1 & 0x7FFFFFu) | 0x3F800000u)};
         }
       };
-      f32x4 rowv{};
-      if constexpr (STAGE) {
-        // this chunk's rows were written to buffer c & 1 during the previous chunk
-        if constexpr (c == 0) {
-          const int bc = b < nb ? b : nb - 1;
-#pragma unroll
-          for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
-          asm volatile("" ::: "memory");
-        }
-        if constexpr (c + 1 < NCH) load_chunk(g, c + 1);
-        else load_chunk(has_next ? g + stride_groups : g, 0);
-        rowv = lds_read_b128<(c & 1) * BUF>(rd_base);
-      } else if constexpr ((ABLATE & kPersistNoMemRandom) != 0) {   // no memory, full-entropy values
+      if constexpr ((ABLATE & kPersistNoMemRandom) != 0) {   // no memory, full-entropy values
         synth_rows();
       } else if constexpr ((ABLATE & kPersistNoMem) != 0) {
         int ln = lane + g;
@@ -506,39 +331,6 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
         for (int x = 0; x < UPR; ++x)
           chunk[x] = f32x4{(float)((ln + x) & 3), (float)((ln + x + 1) & 3), (float)((ln + 2 * x) & 3),
                            (float)((ln ^ x) & 3)};
-      } else if constexpr (LINES) {
-        wait_vmcnt<0>();   // lines c and c + 1 have landed
-        const uint32_t flip = ((c + gp) & 1) * BUF;
-        uint32_t pk[UPR / 2];
-#pragma unroll
-        for (int i = 0; i < UPR / 2; ++i) {
-          pk[i] = rd_pk[i];
-          asm volatile("" : "+v"(pk[i]));   // unpack here, not once for the whole kernel
-        }
-        [&]<int... xs>(std::integer_sequence<int, xs...>) __attribute__((always_inline)) {
-          ((chunk[xs] = lds_read_b128<0>(lds0 + (((xs & 1) ? (pk[xs / 2] >> 16) : (pk[xs / 2] & 0xFFFFu)) ^ flip))),
-           ...);
-        }(std::make_integer_sequence<int, UPR>{});
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(chunk[0]), "+v"(chunk[1]), "+v"(chunk[2]), "+v"(chunk[3]), "+v"(chunk[4]),
-                       "+v"(chunk[5]), "+v"(chunk[6]), "+v"(chunk[7])
-                     :
-                     : "memory");
-        if constexpr (c == 0) {
-          const int bc = b < nb ? b : nb - 1;
-#pragma unroll
-          for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
-          asm volatile("" ::: "memory");
-        }
-        // line c is consumed by every lane: its buffer takes line c + 2, or, after the last window,
-        // both buffers take lines 0 and 1 of the next group (whose line 0 lands in buffer gp ^ 1)
-        if constexpr (c + 2 < NLINE) {
-          issue_line(g, c + 2, (int)((c + gp) & 1));
-        } else {
-          const int gn = has_next ? g + stride_groups : g;
-          issue_line(gn, 0, (int)(gp ^ (NLINE & 1)));
-          issue_line(gn, 1, (int)(gp ^ (NLINE & 1) ^ 1));
-        }
       } else {
         if constexpr (DEPTH2) wait_vmcnt<UPR>();   // the next chunk's may be in flight
         else wait_vmcnt<0>();
@@ -571,20 +363,10 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
       }
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
         constexpr int t = c * PF + u;
-        if constexpr (STAGE) {
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rowv) :: "memory");
-          chunk[u] = rowv;
-          if constexpr (u + 1 < PF) rowv = lds_read_b128<(c & 1) * BUF>(rd_base ^ (uint32_t)((u + 1) * 16));
-          if constexpr (u == PF / 2) {   // the next chunk's units have landed: into the other buffer
-            wait_vmcnt<0>();
-            store_chunk((c + 1) & 1);
-          }
-        }
         const float bm[4] = {chunk[u].x, chunk[u].y, chunk[u].z, chunk[u].w};
         if constexpr (t < G) growth_step<C, t, float>(M, bm, __builtin_inff());
         else if constexpr (t < T) {
           if constexpr ((ABLATE & kPersistSelectAcs) != 0) D[t - G] = acs_step_select<C>(M, bm);
-          else if constexpr (TWINS) D[t - G] = acs_step_twin<C>(M, bm);
           else D[t - G] = acs_step<C, false, float>(M, bm);
           pin(D[t - G]);
         }
@@ -608,9 +390,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
     } else {
       float best;
       const uint32_t st = (uint32_t)argmin_state<S, float>(M, __builtin_inff(), best);
-      uint64_t bits;
-      if constexpr (TWINS) bits = traceback_twin<C.K, BLEN>(D, st, a.blen, reinterpret_cast<const uint8_t*>(twin_pos));
-      else bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
+      const uint64_t bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
       uint64_t ref = 0;
 #pragma unroll
       for (int k = 0; k < IB; ++k) ref |= (uint64_t)info[k] << (56 - 8 * k);
@@ -647,6 +427,18 @@ __device__ __forceinline__ uint32_t lds_read_u8(uint32_t addr) {
   asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
   return r;
 }
+
+// Round-5 A/B switches (build time): per-step scheduling barrier, branch metrics from two
+// popcounts, the next chunk's symbols read one chunk ahead.
+#ifndef CCV_HARD_SCHED_BARRIER
+#define CCV_HARD_SCHED_BARRIER 1
+#endif
+#ifndef CCV_HARD_BM_PAIRS
+#define CCV_HARD_BM_PAIRS 0
+#endif
+#ifndef CCV_HARD_SYM_AHEAD
+#define CCV_HARD_SYM_AHEAD 0
+#endif
 
 template <CodeSpec C, int BLEN, int MMODE = 2>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -713,23 +505,47 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
 #pragma unroll
     for (int s = 0; s < S; ++s) M[s] = MT{(MT)(s ? 0xFF00u : 0u)};   // viterbi-decoder.c:225-228
     DW D[BLEN];
+    constexpr bool AHEAD = CCV_HARD_SYM_AHEAD != 0;
+    uint32_t symq[2][PF];   // AHEAD: chunk c's symbols in symq[c & 1], chunk c + 1's in flight
+    if constexpr (AHEAD) {
+      [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
+        ((symq[0][us] = lds_read_u8<us>(row_addr)), ...);
+      }(std::make_integer_sequence<int, PF>{});
+    }
     auto chunk_at = [&]<int c>() __attribute__((always_inline)) {
       if (c * PF >= a.T) return;   // always true: per-chunk basic blocks (see the soft kernel)
       // inline-asm LDS reads: the compiler would otherwise wait for the NEXT group's DMA (into the
       // other buffer) before every read, since it cannot tell the buffers apart
-      uint32_t sym[PF];
-      [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
-        ((sym[us] = lds_read_u8<c * PF + us>(row_addr)), ...);
-      }(std::make_integer_sequence<int, PF>{});
+      uint32_t* sym = AHEAD ? symq[c & 1] : symq[0];
+      if constexpr (!AHEAD) {
+        [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
+          ((sym[us] = lds_read_u8<c * PF + us>(row_addr)), ...);
+        }(std::make_integer_sequence<int, PF>{});
+      }
       asm volatile("s_waitcnt lgkmcnt(0)"
                    : "+v"(sym[0]), "+v"(sym[1]), "+v"(sym[2]), "+v"(sym[3]), "+v"(sym[4]), "+v"(sym[5]),
                      "+v"(sym[6]), "+v"(sym[7]));
+      if constexpr (AHEAD && c + 1 < NCH) {
+        [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
+          ((symq[(c + 1) & 1][us] = lds_read_u8<(c + 1) * PF + us>(row_addr)), ...);
+        }(std::make_integer_sequence<int, PF>{});
+      }
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
         constexpr int t = c * PF + u;
         if constexpr (t < T) {
           MT BM[NS];
+          if constexpr (CCV_HARD_BM_PAIRS != 0 && NS == 4) {
+            // popcount(k ^ s) over n = 2 bits: k and k ^ 3 sum to 2
+            const uint32_t p0 = (uint32_t)__builtin_popcount(sym[u] & kMask);
+            const uint32_t p1 = (uint32_t)__builtin_popcount((sym[u] ^ 1u) & kMask);
+            BM[0] = (MT)p0;
+            BM[1] = (MT)p1;
+            BM[2] = (MT)(2u - p1);
+            BM[3] = (MT)(2u - p0);
+          } else {
 #pragma unroll
-          for (int k = 0; k < NS; ++k) BM[k] = MT{(MT)__builtin_popcount((uint32_t)k ^ (sym[u] & kMask))};
+            for (int k = 0; k < NS; ++k) BM[k] = MT{(MT)__builtin_popcount((uint32_t)k ^ (sym[u] & kMask))};
+          }
           if constexpr (MMODE == 2) {
 #pragma unroll
             for (int k = 0; k < NS; ++k) asm volatile("" : "+v"(BM[k]));   // else hipcc folds the popcounts into every add (v_bcnt)
@@ -739,7 +555,7 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
             D[t - G] = acs_step<C, false, MT>(M, BM);
             pin(D[t - G]);
           }
-          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (CCV_HARD_SCHED_BARRIER != 0) __builtin_amdgcn_sched_barrier(0);
         }
       };
       [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {

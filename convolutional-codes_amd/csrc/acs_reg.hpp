@@ -84,6 +84,26 @@ __device__ __forceinline__ uint32_t shift_in(uint32_t d, H16 m0, H16 m1) {
   return __builtin_amdgcn_alignbit(d, diff, 31);
 }
 
+// The first of 32 inserts into a word on integer metrics: every bit of the word it starts from is
+// shifted out again, so hipcc drops the opaque zero and turns alignbit(0, m1 - m0, 31) into
+// v_cmp -> VCC -> v_cndmask (a VCC round trip per word per step in the BSC kernels). The sign of
+// m1 - m0 by an explicit full-rate v_lshrrev_b32 instead.
+__device__ __forceinline__ uint32_t first_in(uint16_t m0, uint16_t m1) {
+  uint32_t r;
+  asm("v_lshrrev_b32 %0, 31, %1" : "=v"(r) : "v"((uint32_t)m1 - (uint32_t)m0));
+  return r;
+}
+__device__ __forceinline__ uint32_t first_in(uint32_t m0, uint32_t m1) {
+  uint32_t r;
+  asm("v_lshrrev_b32 %0, 31, %1" : "=v"(r) : "v"(m1 - m0));
+  return r;
+}
+template <typename MT>
+__device__ __forceinline__ uint32_t insert_first(uint32_t d, MT m0, MT m1) {
+  if constexpr (std::is_same_v<MT, uint16_t> || std::is_same_v<MT, uint32_t>) return first_in(m0, m1);
+  else return shift_in(d, m0, m1);
+}
+
 // Insert the decision (m1 < m0) at bit `holes` of (d << (holes + 1)), leaving `holes` don't-care
 // bits below it for positions that are filled by copy_collapsed (v_alignbit takes the top
 // holes + 1 bits of m1 - m0: the sign, then garbage).
@@ -180,7 +200,8 @@ __device__ __forceinline__ DecWord<(1 << (C.K - 1))> acs_step(MT (&M)[1 << (C.K 
   constexpr int H = S / 2;
   MT N[S];
   uint32_t dlo = 0, dhi = 0;
-  if constexpr (std::is_same_v<MT, uint16_t> || std::is_same_v<MT, uint32_t>) {
+  constexpr bool kIntMetric = std::is_same_v<MT, uint16_t> || std::is_same_v<MT, uint32_t>;
+  if constexpr (kIntMetric) {
     // an opaque zero: alignbit(0, m1 - m0, 31) on integer metrics is otherwise folded into
     // v_cmp -> VCC -> v_cndmask (~7 ns per instruction on gfx950, tools/raterbench6.hip)
     asm volatile("" : "+v"(dlo));
@@ -198,9 +219,11 @@ __device__ __forceinline__ DecWord<(1 << (C.K - 1))> acs_step(MT (&M)[1 << (C.K 
         b0 = vmin(b0, (MT)0xFF00); b1 = vmin(b1, (MT)0xFF00);
       }
       N[j] = vmin(a0, a1);
-      dlo = shift_in(dlo, a0, a1);
+      if (kIntMetric && H >= 32 && j == H - 1) dlo = insert_first(dlo, a0, a1);
+      else dlo = shift_in(dlo, a0, a1);
       N[j + H] = vmin(b0, b1);
-      dhi = shift_in(dhi, b0, b1);
+      if (kIntMetric && H >= 32 && j == H - 1) dhi = insert_first(dhi, b0, b1);
+      else dhi = shift_in(dhi, b0, b1);
     }
   } else [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
     ([&]() __attribute__((always_inline)) {
@@ -214,7 +237,8 @@ __device__ __forceinline__ DecWord<(1 << (C.K - 1))> acs_step(MT (&M)[1 << (C.K 
         b0 = vmin(b0, (MT)0xFF00); b1 = vmin(b1, (MT)0xFF00);
       }
       N[j] = vmin(a0, a1);
-      dlo = shift_in(dlo, a0, a1);
+      if constexpr (kIntMetric && H >= 32 && j == H - 1) dlo = insert_first(dlo, a0, a1);
+      else dlo = shift_in(dlo, a0, a1);
       N[j + H] = vmin(b0, b1);
       if constexpr (!collapsed_butterfly<C>(j)) dhi = shift_in_n<collapsed_below<C>(j)>(dhi, b0, b1);
     }(), ...);

@@ -304,9 +304,63 @@ hipError_t launch_service(const ccv::GenericArgs& a, const ccv_plan& p, ccv::Ser
   }
 }
 
+// The achievable-HBM ceiling of the roofline ("a measured copy-kernel ceiling"): a
+// streaming pass over a buffer in 16-byte lanes, four global_load_dwordx4 in flight per lane, each
+// wave-instruction 1 KiB of consecutive bytes. COPY stores every vector (global_store_dwordx4: the
+// float4 copy of MI355X_MICROARCH.md, 6.29 TB/s read + write there); otherwise the loads are folded
+// into one XOR per lane so nothing is stored but a never-taken sink write (read-only stream, the
+// access the decode kernels make of their input).
+template <bool COPY>
+__global__ __launch_bounds__(256) void hbm_stream(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                  size_t n16, uint32_t* sink) {
+  constexpr int U = 4;
+  const size_t stride = (size_t)gridDim.x * 256 * U;
+  uint32_t acc = 0;
+  size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+  for (; i + (U - 1) * 256 < n16; i += stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (COPY) dst[i + u * 256] = v[u];
+      else acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+  }
+  for (; i < n16; i += 256) {   // the ragged end of the buffer
+    const uint4 v = src[i];
+    if constexpr (COPY) dst[i] = v;
+    else acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (!COPY && acc == 0x9E3779B9u && sink) sink[0] = acc;   // keeps the loads live
+}
+
 }  // namespace
 
 extern "C" {
+
+int ccv_hbm_probe(int mode, void* dst, const void* src, size_t bytes, uint32_t* sink, void* stream) {
+  if (mode != 0 && mode != 1) return fail("ccv_hbm_probe: mode must be 0 (copy) or 1 (read)");
+  if (!src || (mode == 0 && !dst)) return fail("ccv_hbm_probe: null buffer");
+  if (((uintptr_t)src | (uintptr_t)dst | bytes) & 15) return fail("ccv_hbm_probe: 16-byte alignment");
+  const size_t n16 = bytes / 16;
+  if (n16 == 0) return 0;
+  int dev = 0, cus = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  // 8 workgroups of 4 waves per CU: 32 waves per CU, 16 KiB of loads in flight per wave
+  const size_t want = (n16 + 1023) / 1024;
+  const unsigned grid = (unsigned)(want < (size_t)cus * 8 ? want : (size_t)cus * 8);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (mode == 0)
+    hipLaunchKernelGGL((hbm_stream<true>), dim3(grid), dim3(256), 0, s, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), n16, sink);
+  else
+    hipLaunchKernelGGL((hbm_stream<false>), dim3(grid), dim3(256), 0, s, static_cast<const uint4*>(src),
+                       nullptr, n16, sink);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
 
 const char* ccv_last_error(void) { return g_last_error.c_str(); }
 

@@ -410,6 +410,9 @@ __device__ __forceinline__ void row_min_min_u32_swz(uint32_t& a, uint32_t& b) {
 #ifndef CCV_STACK_SYMG
 #define CCV_STACK_SYMG 0
 #endif
+#ifndef CCV_STACK_SGPR_SEL
+#define CCV_STACK_SGPR_SEL 0
+#endif
 __host__ __device__ constexpr size_t stack_rows_sym_bytes(int T, int ns, bool hard) {
   if (CCV_STACK_SYMG && !hard) return 0;
   return (((size_t)T * (size_t)ns * (hard ? 1 : 4)) + 15) & ~(size_t)15;
@@ -554,10 +557,47 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
         else row_max_min<RL>(mx, mn);
         uint32_t cand = kStackDepth;
         c2 = kStackDepth;
+        if constexpr (CCV_STACK_SGPR_SEL && kRowSlots == 4) {
+          // the eight compares into SGPR pairs first, then the selects: hipcc's form is a serial
+          // v_cmp -> VCC -> v_cndmask_e32 chain with an s_nop 1 in each link (2 wait states after a
+          // VALU SGPR write on gfx950), and a VCC compare/select pair costs ~7 ns per instruction
+          // (profiles/r02_rates_argmin.txt). Here every select reads a mask written >= 2 VALU
+          // instructions earlier: no wait state, no VCC. Same result: the lowest k with
+          // met[k] == mx (resp. mn) wins.
+          const uint32_t i0 = (uint32_t)(l * kRowSlots);
+          uint64_t e0, e1, e2, e3, f0, f1, f2, f3;
+          uint32_t tmp;
+          asm volatile(
+              "v_cmp_eq_f32_e64 %[e3], %[m3], %[mx]\n"
+              "v_cmp_eq_f32_e64 %[f3], %[m3], %[mn]\n"
+              "v_cmp_eq_f32_e64 %[e2], %[m2], %[mx]\n"
+              "v_cmp_eq_f32_e64 %[f2], %[m2], %[mn]\n"
+              "v_cmp_eq_f32_e64 %[e1], %[m1], %[mx]\n"
+              "v_cmp_eq_f32_e64 %[f1], %[m1], %[mn]\n"
+              "v_cmp_eq_f32_e64 %[e0], %[m0], %[mx]\n"
+              "v_cmp_eq_f32_e64 %[f0], %[m0], %[mn]\n"
+              "v_add_u32 %[t], 3, %[i0]\n"
+              "v_cndmask_b32_e64 %[c], 64, %[t], %[e3]\n"
+              "v_cndmask_b32_e64 %[d], 64, %[t], %[f3]\n"
+              "v_add_u32 %[t], 2, %[i0]\n"
+              "v_cndmask_b32_e64 %[c], %[c], %[t], %[e2]\n"
+              "v_cndmask_b32_e64 %[d], %[d], %[t], %[f2]\n"
+              "v_add_u32 %[t], 1, %[i0]\n"
+              "v_cndmask_b32_e64 %[c], %[c], %[t], %[e1]\n"
+              "v_cndmask_b32_e64 %[d], %[d], %[t], %[f1]\n"
+              "v_cndmask_b32_e64 %[c], %[c], %[i0], %[e0]\n"
+              "v_cndmask_b32_e64 %[d], %[d], %[i0], %[f0]\n"
+              : [e0] "=&s"(e0), [e1] "=&s"(e1), [e2] "=&s"(e2), [e3] "=&s"(e3), [f0] "=&s"(f0),
+                [f1] "=&s"(f1), [f2] "=&s"(f2), [f3] "=&s"(f3), [c] "=&v"(cand), [d] "=&v"(c2),
+                [t] "=&v"(tmp)
+              : [m0] "v"(met[0]), [m1] "v"(met[1]), [m2] "v"(met[2]), [m3] "v"(met[3]), [mx] "v"(mx),
+                [mn] "v"(mn), [i0] "v"(i0));
+        } else {
 #pragma unroll
-        for (int k = kRowSlots - 1; k >= 0; --k) {
-          cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
-          c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
+          for (int k = kRowSlots - 1; k >= 0; --k) {
+            cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
+            c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
+          }
         }
         if constexpr (CCV_STACK_SWZ) row_min_min_u32_swz<RL>(cand, c2);
         else row_min_min_u32<RL>(cand, c2);

@@ -182,6 +182,12 @@ int ccv_stack_decode_host(ccv_plan* plan, const void* in, size_t nblocks, const 
 int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out,
                     int32_t* path_metric);
 
+/* Achievable-HBM probe for the roofline (bench.py): one streaming pass over `bytes` (a multiple of
+ * 16, 16-byte aligned buffers) with global_load_dwordx4 -- mode 0 copies src to dst
+ * (global_store_dwordx4; read + write bytes move), mode 1 only reads src (sink: a 4-byte device
+ * word the kernel never writes in practice, or NULL). Launched on `stream`; time it with events. */
+int ccv_hbm_probe(int mode, void* dst, const void* src, size_t bytes, uint32_t* sink, void* stream);
+
 /* Number of visible HIP devices (0 without a GPU; never fails). */
 int ccv_device_count(void);
 

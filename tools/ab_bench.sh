@@ -11,7 +11,7 @@ for rep in $(seq 1 ${REPS:-3}); do
   for name in "$@"; do
     if [ "$name" = head ]; then dir=$PWD/convolutional-codes_amd/lib; else dir=$PWD/convolutional-codes_amd/build_ab/$name/lib; fi
     log=gpurun_out/ab/${TAG:-ab}_${name}_$rep.log
-    CCV_LIB_DIR=$dir timeout -k 10 300 python bench.py $ARGS --no-cpu-baseline --no-fused-channel > $log 2>&1 \
+    CCV_LIB_DIR=$dir timeout -k 10 300 python bench.py $ARGS --no-cpu-baseline --no-fused-channel --no-hbm-probe > $log 2>&1 \
         || { echo "$name failed"; tail -5 $log; exit 1; }
     python3 -c "
 import json; d=json.loads(open('$log').read().strip().splitlines()[-1])

@@ -119,13 +119,11 @@ int ab(RegArgs a, int ng, int cus, bool only_first = false) {
   auto A = [&]() { return sustained<kK7Ref, 0>(a, ng, 8, cus, 40); };
   struct V { const char* name; float (*f)(RegArgs, int, int, int, int); bool b42; };
   const V vs_all[] = {
-    {"twin classes (one decision per class)", sustained<kK7Ref, kPersistTwins>, false},
     {"input nt (aux 2)", sustained<kK7Ref, kPersistInputNt>, false},
     {"2-deep DMA", sustained<kK7Ref, kPersistDepth2>, false},
     {"no DMA (stale LDS rows)", sustained<kK7Ref, kPersistNoDma>, false},
     {"DMA, no LDS reads (synth)", sustained<kK7Ref, kPersistNoLdsRead>, false},
     {"no memory, synth rows", sustained<kK7Ref, kPersistNoMem | kPersistNoMemRandom>, false},
-    {"line-aligned", sustained<kK7Ref, kPersistLineChunks>, false},
     {"blen42 aligned (per bit)", sustained<kK7Ref, 0, 42>, true},
     {"L2-resident input", sustained<kK7Ref, kPersistCachedInput>, false},
     {"no traceback", sustained<kK7Ref, kPersistNoTraceback>, false},
@@ -245,7 +243,6 @@ int main(int argc, char** argv) {
     run<kK7Ref, kPersistNoTraceback>("ref no-traceback", a, ng, w, cus);
     run<kK7Ref, kPersistNoMem | kPersistNoTraceback>("ref no-mem no-traceback", a, ng, w, cus);
   }
-  run<kK7Ref, kPersistLineChunks>("ref full, line-aligned chunks", a, ng, 8, cus);
   run<kK7Ref, kPersistDepth2>("ref full, 2-deep double-buffered DMA", a, ng, 8, cus);
   {   // blen 42: T = 48, a block is exactly 6 x 128-byte lines -> no chunk straddles a line
     RegArgs a42 = a;

@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-5 GPU sessions, one function per gpurun call: tools/r05_session.sh PHASE.
+# Every GPU step runs under its own time limit; the first failure ends the session (set -e).
+# Logs in gpurun_out/r05<phase>/ (what is judged is copied to profiles/).
+set -eu
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp PYTHONPATH=$PWD/convolutional-codes_amd
+AB=$PWD/convolutional-codes_amd/build_ab
+PYT="python -u -m pytest -q -p no:cacheprovider --timeout 300 --timeout-method thread"
+
+show() {   # one-line summary of a bench JSON log
+  python3 -c "
+import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']
+print(sys.argv[1].split('/')[-1], d['value'], 'kernel_ms', d['kernel_ms'],
+      'copy', r.get('hbm_copy_gbs'), 'read', r.get('hbm_read_gbs'), 'frac', r.get('frac'))" "$1"
+}
+
+# a: the BSC K=7 first-decision fix and its three A/B switches; the stack decoder's SGPR-mask
+# selects, swizzle reductions at 31 waves per CU, and both; the full GPU suite on the new tree.
+phase_a() {
+  O=gpurun_out/r05a; mkdir -p $O
+  timeout -k 10 900 $PYT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+  tail -n 2 $O/pytest_gpu.log
+  for v in sel selswzg; do
+    CCV_LIB_DIR=$AB/$v/lib timeout -k 10 600 $PYT tests/test_gpu_stack.py > $O/pytest_stack_$v.log 2>&1 \
+      || { tail -20 $O/pytest_stack_$v.log; exit 1; }
+    echo "stack tests $v: $(tail -n 1 $O/pytest_stack_$v.log)"
+  done
+  timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_k7.log 2>&1; show $O/bench_k7.log
+  REPS=3 TAG=bsc tools/ab_bench.sh "--channel bsc" r04 head hnb hbm hsa
+  REPS=2 TAG=stack tools/ab_bench.sh "--decoder stack --frames 16 --steps 5 --warmup 1" head sel swzg selswzg
+  REPS=2 TAG=stackbsc tools/ab_bench.sh "--decoder stack --channel bsc --frames 16 --steps 5 --warmup 1" head swzg
+  mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
+}
+
+"phase_$1"
