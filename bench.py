@@ -243,8 +243,6 @@ def pmc_for_variant(pmc, variant):
         return pmc if "viterbi_wide_persist" in kernel else {}
     if variant == "persistent-slot2":
         return pmc if "viterbi_multi2_slot" in kernel else {}
-    if variant == "persistent-slot4":
-        return pmc if "viterbi_multi_slot" in kernel else {}
     if variant == "persistent":
         return pmc if "_persist<" in kernel and "wide" not in kernel else {}
     return pmc

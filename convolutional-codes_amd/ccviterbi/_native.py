@@ -94,8 +94,14 @@ def core():
     L.ccv_fano_decode_device.restype = _i
     L.ccv_decode_host.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.ccv_decode_host.restype = _i
-    L.ccv_hbm_probe.argtypes = [_i, _vp, _vp, _sz, _vp, _vp]
-    L.ccv_hbm_probe.restype = _i
+    # entry points added in round 5: bound where present, so the libraries of an older revision
+    # (whole-build A/B, tools/ab_build.sh) still load; calling one that is absent raises
+    if hasattr(L, "ccv_plan_set_option"):
+        L.ccv_plan_set_option.argtypes = [_vp, ctypes.c_char_p, ctypes.c_longlong]
+        L.ccv_plan_set_option.restype = _i
+    if hasattr(L, "ccv_hbm_probe"):
+        L.ccv_hbm_probe.argtypes = [_i, _vp, _vp, _sz, _vp, _vp]
+        L.ccv_hbm_probe.restype = _i
     L.ccv_device_count.argtypes = []
     L.ccv_device_count.restype = _i
     L.ccv_last_error.argtypes = []

@@ -100,6 +100,12 @@ class Plan:
         self._lib.ccv_plan_trellis(self._h, out.ctypes.data)
         return out
 
+    def set_option(self, name: str, value: int):
+        """ccv_plan_set_option: a per-plan kernel A/B switch (include/ccv.h lists them); returns self."""
+        if self._lib.ccv_plan_set_option(self._h, name.encode(), int(value)) != 0:
+            raise DecoderError(f"ccv_plan_set_option: {_native.last_error()}")
+        return self
+
     def reserve(self, max_blocks: int):
         if self._lib.ccv_plan_reserve(self._h, max_blocks) != 0:
             raise DecoderError(f"ccv_plan_reserve: {_native.last_error()}")

@@ -135,17 +135,24 @@ class DeviceChannelDecoder:
             self.d_out = torch.empty((self.chunk, code.out_bytes), dtype=torch.uint8, device=self.device)
             self.d_pm = torch.empty(self.chunk, dtype=torch.int32, device=self.device)
 
-    def warm_up(self, seconds: float) -> int:
-        """Decode throw-away chunks (blocks 2^62.., a Philox range no point uses) for `seconds`: the
-        first call's scratch allocation and the GPU's clock ramp (~35 ms of load)
-        then stay out of the first point's time. Returns the chunks run."""
+    def warm_up(self, seconds: float, point: Optional[float] = None) -> int:
+        """Decode throw-away slices (blocks 2^62.., a Philox range no point uses) until `seconds` have
+        passed: the GPU's clock ramp (~35 ms of load) and the first launches then stay
+        out of the first point's time. A slice is a few frames (one frame for the stack / Fano
+        decoders), so the limit is kept to within one slice. The Viterbi kernels run at `point` (the
+        sweep's first point; their time does not depend on the noise); the sequential decoders at a
+        low-noise point (10 dB / 1,000 ppm), where no search runs into its timeout. Returns the
+        slices run."""
         import time
+        seq = self.seq is not None
+        if seq or point is None:
+            point = (10.0 if seq else 4.0) if self.channel == SOFT else (1000 if seq else 50000)
+        nb = min(self.chunk, self.frame_blocks * (1 if seq else 4))
         n, t0 = 0, time.perf_counter()
-        while True:
-            self(4.0 if self.channel == SOFT else 50000, 1 << 62, self.chunk)
+        while n == 0 or time.perf_counter() - t0 < seconds:
+            self(point, 1 << 62, nb)
             n += 1
-            if time.perf_counter() - t0 >= seconds:
-                return n
+        return n
 
     def __call__(self, point: float, first_block: int, nblocks: int) -> int:
         """Bit errors of blocks first_block .. first_block + nblocks - 1 at Eb/N0 (dB) or p_ppm `point`."""
@@ -341,7 +348,7 @@ def main(argv=None, decode=None):
             dev = DeviceChannelDecoder(code, channel, args.frame_blocks, args.seed,
                                        hard_demap=args.hard_demap, decoder=args.decoder)
             if args.warmup > 0:
-                dev.warm_up(args.warmup)
+                dev.warm_up(args.warmup, points[0] if points else None)
         else:
             gpu = GpuFrameDecoder(code, channel, args.frame_blocks, decoder=args.decoder)
     counters = np.zeros((len(points), 2), np.int64)

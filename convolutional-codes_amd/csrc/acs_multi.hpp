@@ -176,83 +176,6 @@ __device__ __forceinline__ uint32_t swz_quad_u32(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, pat);
 }
 
-// Cross-lane phase P (X::is_lane(P)) of the four-lane slot kernel with the predecessors fetched by
-// ds_swizzle instead of DPP: registers in chunks of G, the swizzles of chunk c + 1 issued before the
-// ACS of chunk c so their LDS-unit latency overlaps it. Same values, same decision bits (register R
-// at bit R of hi:lo, descending) as multi_acs.
-template <CodeSpec C, int P, class X, int G = 8>
-__device__ __forceinline__ uint64_t multi_cross_swz(float (&M)[64], const float (&BM)[1 << C.n], bool qb0,
-                                                    bool qb1) {
-  static_assert(X::is_lane(P), "cross-lane phase");
-  constexpr int B = X::lane_of(P);
-  constexpr int L = X::L;
-  constexpr int NC = 64 / G;
-  float E[2][G], O[2][G];
-  auto issue = [&]<int c>() __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const int R = 63 - (c * G + i);
-      if constexpr (B == 0) {
-        E[c & 1][i] = swz_quad<0, 0, 2, 2>(M[R]);
-        O[c & 1][i] = swz_quad<1, 1, 3, 3>(M[R]);
-      } else {
-        E[c & 1][i] = swz_quad<0, 1, 0, 1>(M[R]);
-        O[c & 1][i] = swz_quad<2, 3, 2, 3>(M[R]);
-      }
-    }
-  };
-  uint32_t lo = 0, hi = 0;
-  auto compute = [&]<int c>() __attribute__((always_inline)) {
-    [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
-      ([&]() __attribute__((always_inline)) {
-        constexpr int R = 63 - (c * G + is);
-        constexpr auto e = [](int q, int odd) {
-          const int qe = q & ~(1 << B);
-          return expected_symbol(C, X::logical(qe, R, P) | (uint32_t)odd, (q >> B) & 1);
-        };
-        const float a0 = E[c & 1][is] + select_bm<L, e(0, 0), e(1 % L, 0), e(2 % L, 0), e(3 % L, 0)>(BM, qb0, qb1);
-        const float a1 = O[c & 1][is] + select_bm<L, e(0, 1), e(1 % L, 1), e(2 % L, 1), e(3 % L, 1)>(BM, qb0, qb1);
-        M[R] = vmin(a0, a1);
-        if constexpr (R >= 32) hi = shift_in(hi, a0, a1);
-        else lo = shift_in(lo, a0, a1);
-      }(), ...);
-    }(std::make_integer_sequence<int, G>{});
-  };
-  issue.template operator()<0>();
-  [&]<int... cs>(std::integer_sequence<int, cs...>) __attribute__((always_inline)) {
-    ([&]() __attribute__((always_inline)) {
-      if constexpr (cs + 1 < NC) issue.template operator()<cs + 1>();
-      __builtin_amdgcn_sched_barrier(0);
-      compute.template operator()<cs>();
-      __builtin_amdgcn_sched_barrier(0);
-    }(), ...);
-  }(std::make_integer_sequence<int, NC>{});
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// Growth cross-lane phase through ds_swizzle (the slot kernel's XSWZ form of multi_growth): every
-// new state is its even predecessor, fetched from the pair's lane with the lane bit clear, plus the
-// branch metric.
-template <CodeSpec C, int P, class X>
-__device__ __forceinline__ void multi_growth_cross_swz(float (&M)[64], const float (&BM)[1 << C.n], bool qb0,
-                                                       bool qb1) {
-  static_assert(X::is_lane(P), "cross-lane phase");
-  constexpr int B = X::lane_of(P);
-  constexpr int L = X::L;
-  float E[64];
-#pragma unroll
-  for (int R = 0; R < 64; ++R) E[R] = B == 0 ? swz_quad<0, 0, 2, 2>(M[R]) : swz_quad<0, 1, 0, 1>(M[R]);
-  [&]<int... Rs>(std::integer_sequence<int, Rs...>) __attribute__((always_inline)) {
-    ([&]() __attribute__((always_inline)) {
-      constexpr auto e = [](int q) {
-        const int qe = q & ~(1 << B);
-        return expected_symbol(C, X::logical(qe, Rs, P), (q >> B) & 1);
-      };
-      M[Rs] = E[Rs] + select_bm<L, e(0), e(1 % L), e(2 % L), e(3 % L)>(BM, qb0, qb1);
-    }(), ...);
-  }(std::make_integer_sequence<int, 64>{});
-}
-
 // Growth step (t = P < K-1, from the reset metrics): the odd predecessor of every state is still
 // unreachable (its candidate is +inf / saturated 0xFF00 and never wins the strict compare), so each
 // new state is its even predecessor plus the branch metric and its decision is 0 -- the adds only
@@ -844,218 +767,6 @@ void viterbi_multi_persist(RegArgs a, int ngroups) {
       }(std::make_integer_sequence<int, NPER>{});
       bits = __builtin_bitreverse64(h);   // bit 63 - t = output of step t
     }
-    if (q == 0 && blk < nb) {
-      uint8_t* o = a.out + (size_t)blk * OB;
-#pragma unroll
-      for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
-      if (a.info != nullptr) {   // consumer AWGN-channel/main.c:118-144
-        uint64_t ref = 0;
-#pragma unroll
-        for (int k = 0; k < IB; ++k) ref |= (uint64_t)info[k] << (56 - 8 * k);
-        constexpr uint64_t mask = BLEN >= 64 ? ~0ull : ~(~0ull >> BLEN);
-        errors += (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
-      }
-    }
-  }
-  wait_vmcnt<0>();   // the look-ahead DMA writes LDS: it must land before the workgroup ends
-  accumulate_errors(a, errors);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Persistent K = 9 soft kernel with the main periods as a LOOP (round 4; production path of the
-// textbook (561,753) code, whose 256 metrics are all distinct). viterbi_multi_persist above is fully
-// unrolled: six periods of 8 phases x 64 registers are 76 KB of code for the true-parity trellis
-// (65 KB for the idiom one), past the instruction cache -- its waves were issue-stalled 46 % of their
-// lifetime at valu_frac 0.51 (profiles/pmc_workloads.json k9:true:frames32:block), the same
-// starvation the one-lane kernel measured fully unrolled (acs_wide.hpp). Here only the growth
-// period is unrolled and the five main periods run one 8-phase body, so the decision words cannot
-// live in statically indexed registers: each step's 64-bit word goes straight to a per-wave scratch
-// slot ([main step][lane] 8-byte words, 20 KiB per wave, rewritten by every group the wave decodes,
-// so it stays in the L2 / Infinity-Cache working set) with one buffer store. The traceback first
-// drains those stores (vmcnt(0): acknowledged by L2) and reads them back with agent-scope loads (sc1:
-// they miss the CU's L1, which may hold the previous group's lines), a period at a time, two in
-// flight, then walks them exactly as viterbi_multi_persist does (physical coordinates, quad DPP).
-// Same arithmetic as viterbi_multi_persist: bit-identical outputs.
-template <CodeSpec C, int BLEN, int LB0 = 0, int LB1 = 3>
-constexpr size_t multi_slot_bytes() {
-  return (size_t)(BLEN + C.K - 1 - (C.K - 1)) * kRegThreads * 8;   // main steps x 64 lanes x 8 B
-}
-
-#ifndef CCV_SLOT_GROUP
-#define CCV_SLOT_GROUP 0
-#endif
-template <CodeSpec C, int BLEN, int WAVES = 3, bool XSWZ = false, int LB0 = 0, int LB1 = 3>
-__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(WAVES)))
-void viterbi_multi_slot(RegArgs a, int ngroups) {
-  using X = Multi<C, LB0, LB1>;
-  using MT = float;
-  static_assert(C.K == 9 && C.n == 2, "K = 9, r = 1/2: the period (8 steps) is the 8-step chunk");
-  constexpr int n = X::n;                     // 8 phases per period
-  constexpr int T = BLEN + C.K - 1;
-  static_assert(T % n == 0 && T / n >= 2 && T / n <= 7, "whole periods");
-  constexpr int NPER = T / n;                 // periods = chunks
-  constexpr int NMAIN = NPER - 1;             // periods with decisions
-  constexpr int BPG = kRegThreads / X::L;     // blocks per group (16)
-  constexpr int ROWB = n * 16;                // one chunk of one block: 128 bytes
-  constexpr int BUF = BPG * ROWB;             // 2 KiB
-  constexpr int UNITS = BUF / 16;             // 16-byte DMA units per chunk (128: 2 instructions)
-  constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
-  constexpr uint32_t block_bytes = (uint32_t)T * 16;
-  constexpr int STEPB = kRegThreads * 8;      // slot bytes per main step
-  static_assert(multi_slot_bytes<C, BLEN, LB0, LB1>() == (size_t)NMAIN * n * STEPB, "slot layout");
-  const int lane = threadIdx.x;
-  const int q = lane & (X::L - 1);
-  const bool qb0 = (q & 1) != 0, qb1 = (q & 2) != 0;
-  const int nb = a.nblocks;
-  const int stride_groups = gridDim.x;
-  // two chunk buffers: chunk c lives in buffer c % 2 (NPER is even, so the parity carries across
-  // groups); a chunk's rows are read from LDS one step ahead, never held for the whole period, and the
-  // next chunk's DMA goes into the other buffer as soon as this one's has landed
-  static_assert(NPER % 2 == 0, "buffer = chunk parity across groups");
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
-  const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
-  auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < UNITS / kRegThreads; ++k) {
-      const int unit = k * kRegThreads + lane;
-      const int r = unit / n, j = unit % n;
-      const int gb = g * BPG + r < nb ? g * BPG + r : nb - 1;
-      __builtin_amdgcn_global_load_lds(in + (size_t)gb * block_bytes + (uint32_t)(c * n + j) * 16,
-                                       (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16), 16, 0, 0);
-    }
-  };
-  const uint32_t row = (uint32_t)(uintptr_t)(lds_ptr_t)lds + (uint32_t)((lane / X::L) * ROWB);
-  const uint8_t* info_src = a.info != nullptr ? a.info : reinterpret_cast<const uint8_t*>(a.in);
-  const int info_stride = a.info != nullptr ? IB : 0;
-  const __amdgpu_buffer_rsrc_t slot = __builtin_amdgcn_make_buffer_rsrc(
-      static_cast<unsigned char*>(a.dec) + (size_t)blockIdx.x * NMAIN * n * STEPB, 0, NMAIN * n * STEPB,
-      0x00020000);
-  const int col = lane * 8;
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  constexpr int kSc1 = 16;   // cache policy: agent scope (sc1), the load misses the CU's L1
-
-  uint32_t errors = 0;
-  int g = blockIdx.x;
-  if (g < ngroups) issue_chunk(g, 0, 0);
-  for (; g < ngroups; g += stride_groups) {
-    const int blk = g * BPG + lane / X::L;
-    const bool has_next = g + stride_groups < ngroups;
-    MT M[64];
-#pragma unroll
-    for (int r = 0; r < 64; ++r) M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
-    uint8_t info[IB];
-    // period p: wait for the chunk's DMA, start the next one into the other buffer, eight phases
-    // reading each step's row one step ahead
-    auto period_at = [&](int p, auto growth) __attribute__((always_inline)) {
-      constexpr bool GROWTH = decltype(growth)::value;
-      // this chunk's DMA was issued before the previous period's 8 decision stores (in order)
-      if (p >= 2) wait_vmcnt<n>();
-      else wait_vmcnt<0>();
-      if constexpr (GROWTH) {
-        const int bc = blk < nb ? blk : nb - 1;
-#pragma unroll
-        for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
-        asm volatile("" ::: "memory");   // info loads before the DMA (vmcnt order)
-      }
-      const int buf = p & 1;
-      if (p + 1 < NPER) issue_chunk(g, p + 1, buf ^ 1);
-      else issue_chunk(has_next ? g + stride_groups : g, 0, buf ^ 1);
-      const uint32_t rd = row + (uint32_t)(buf * BUF);
-      f32x4 rowv = lds_read_b128<0>(rd);
-      auto phase_at = [&]<int P>() __attribute__((always_inline)) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rowv) :: "memory");
-        const MT BM[4] = {rowv.x, rowv.y, rowv.z, rowv.w};
-        if constexpr (P + 1 < n) rowv = lds_read_b128<(P + 1) * 16>(rd);
-        if constexpr (GROWTH) {
-          if constexpr (X::is_lane(P) && XSWZ)
-            multi_growth_cross_swz<C, P, X>(M, BM, qb0, qb1);
-          else
-            multi_growth_step_impl<C, P, false, MT, X>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
-        } else {
-          uint64_t w;
-          if constexpr (X::is_lane(P) && XSWZ)   // cross-lane phase through the LDS crossbar
-            w = multi_cross_swz<C, P, X>(M, BM, qb0, qb1);
-          else
-            w = multi_step_impl<C, P, false, MT, X, CCV_SLOT_GROUP>(M, BM, qb0, qb1, std::make_index_sequence<64>{});
-          __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)w, (uint32_t)(w >> 32)}, slot, col,
-                                                ((p - 1) * n + P) * STEPB, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
-        (phase_at.template operator()<Ps>(), ...);
-      }(std::make_integer_sequence<int, n>{});
-    };
-    period_at(0, std::true_type{});
-#pragma clang loop unroll(disable)
-    for (int p = 1; p < NPER; ++p) period_at(p, std::false_type{});
-
-    MT best;
-    static_assert(T % n == 0, "the persistent trellis ends on phase 0");
-    const uint32_t st = multi_argmin_phase0<C, X>(M, q, __builtin_inff(), best);
-    // Traceback in physical coordinates (viterbi_multi_persist): the walk keeps the slot's lane part
-    // ql and register part rl; each lane of the quad extracts its own word's candidate bit and two
-    // quad DPP ORs give every lane all four, from which it takes lane ql's.
-    uint32_t ql = 0, rl = 0;
-    {
-      int k = 0;
-#pragma unroll
-      for (int b = 0; b < n; ++b) {
-        if (X::is_lane(b)) ql |= ((st >> b) & 1u) << X::lane_of(b);
-        else rl |= ((st >> b) & 1u) << k++;
-      }
-    }
-    uint64_t h = st;
-    const uint32_t qself = (uint32_t)q;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this group's decision stores reached L2
-    uint64_t dw[2][n];
-    auto load_period = [&]<int pp>() __attribute__((always_inline)) {   // main period pp (1-based)
-#pragma unroll
-      for (int P = 0; P < n; ++P) {
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(slot, col, ((pp - 1) * n + P) * STEPB, kSc1);
-        dw[pp & 1][P] = ((uint64_t)v.y << 32) | v.x;
-      }
-    };
-    auto walk_period = [&]<int pp>() __attribute__((always_inline)) {
-      [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
-        ([&]() __attribute__((always_inline)) {
-          constexpr int P = n - 1 - Ps;
-          uint32_t pos;
-          if constexpr (X::is_lane(P)) pos = rl;
-          else pos = multi_dec_pos_k(rl, X::reg_bit(P));
-          const uint32_t own = (uint32_t)(dw[pp & 1][P] >> pos) & 1u;
-          uint32_t m = own << qself;
-          if constexpr (XSWZ) {   // through the LDS crossbar (no cross-lane VALU, see swz_quad)
-            m |= swz_quad_u32<1, 0, 3, 2>(m);
-            m |= swz_quad_u32<2, 3, 0, 1>(m);
-          } else {
-            m |= dpp_u32<0xB1>(m);   // quad_perm [1,0,3,2]
-            m |= dpp_u32<0x4E>(m);   // quad_perm [2,3,0,1]
-          }
-          const uint32_t d = (m >> ql) & 1u;
-          if constexpr (X::is_lane(P)) {
-            constexpr uint32_t bit = 1u << X::lane_of(P);
-            ql = (ql & ~bit) | (d << X::lane_of(P));
-          } else {
-            constexpr uint32_t bit = 1u << X::reg_bit(P);
-            rl = (rl & ~bit) | (d << X::reg_bit(P));
-          }
-          h = (h << 1) | d;
-        }(), ...);
-      }(std::make_integer_sequence<int, n>{});
-    };
-    static_assert(NMAIN == 5, "K = 9 at blen 40: five main periods");
-    load_period.template operator()<5>();
-    load_period.template operator()<4>();
-    walk_period.template operator()<5>();
-    load_period.template operator()<3>();
-    walk_period.template operator()<4>();
-    load_period.template operator()<2>();
-    walk_period.template operator()<3>();
-    load_period.template operator()<1>();
-    walk_period.template operator()<2>();
-    walk_period.template operator()<1>();
-    const uint64_t bits = __builtin_bitreverse64(h);   // bit 63 - t = output of step t
     if (q == 0 && blk < nb) {
       uint8_t* o = a.out + (size_t)blk * OB;
 #pragma unroll

@@ -88,15 +88,7 @@ __device__ __forceinline__ void multi2_acs(float (&M)[X::NR], const float (&BM)[
       D[2 + (c >> 5)] = shift_in(D[2 + (c >> 5)], b0, b1);
     }
   } else {
-    // cross-lane butterfly: even predecessor in the pair's lane 0, odd in lane 1, same register; this
-    // lane's new state has input bit = its own lane bit
-    constexpr auto e = [](int q, int odd) { return expected_symbol(C, X::logical(0, R, P) | (uint32_t)odd, q); };
-    const float E = dpp<0xA0, float>(M[R]);   // quad_perm [0,0,2,2]
-    const float O = dpp<0xF5, float>(M[R]);   // quad_perm [1,1,3,3]
-    const float a0 = E + select_bm<2, e(0, 0), e(1, 0), 0, 0>(BM, qb, false);
-    const float a1 = O + select_bm<2, e(0, 1), e(1, 1), 0, 0>(BM, qb, false);
-    M[R] = vmin(a0, a1);
-    D[R >> 5] = shift_in(D[R >> 5], a0, a1);
+    static_assert(!X::is_lane(P), "the cross phase runs in multi2_cross_swz");
   }
 }
 
@@ -115,12 +107,11 @@ __device__ __forceinline__ void multi2_growth(float (&M)[X::NR], const float (&B
       M[R1] = even + select_bm<2, e(0, 1), e(1, 1), 0, 0>(BM, qb, false);
     }
   } else {
-    constexpr auto e = [](int q) { return expected_symbol(C, X::logical(0, R, P), q); };
-    M[R] = dpp<0xA0, float>(M[R]) + select_bm<2, e(0), e(1), 0, 0>(BM, qb, false);
+    static_assert(!X::is_lane(P), "the growth cross phase runs in multi2_growth_cross_swz");
   }
 }
 
-// The cross phase through ds_swizzle (XSWZ; acs_multi.hpp multi_cross_swz): any DPP / permlane /
+// The cross phase through ds_swizzle: any DPP / permlane /
 // readlane VALU instruction drops the wave's whole VALU stream to about half rate for ~800
 // instructions on gfx950, and the cross phase issues 256 of them per period, so the
 // even / odd predecessors come from the pair's lanes through the LDS crossbar instead -- registers in
@@ -167,7 +158,7 @@ __device__ __forceinline__ void multi2_cross_swz(float (&M)[X::NR], const float 
   }(std::make_integer_sequence<int, NC>{});
 }
 
-// Growth cross phase through ds_swizzle (XSWZ): every new state is its even predecessor (the pair's
+// Growth cross phase through ds_swizzle: every new state is its even predecessor (the pair's
 // lane 0, same register) plus the branch metric, in chunks of G registers.
 template <CodeSpec C, int P, class X, int G = CCV_MULTI2_XG>
 __device__ __forceinline__ void multi2_growth_cross_swz(float (&M)[X::NR], const float (&BM)[4], bool qb) {
@@ -190,21 +181,10 @@ __device__ __forceinline__ void multi2_growth_cross_swz(float (&M)[X::NR], const
   }(std::make_integer_sequence<int, NR / G>{});
 }
 
-// the pair's other lane (quad_perm [1,0,3,2]) -- ds_swizzle with XSWZ, DPP otherwise (the argmin and
-// the traceback; CCV_MULTI2_MISC_DPP=1 keeps DPP there for A/B)
-#ifndef CCV_MULTI2_MISC_DPP
-#define CCV_MULTI2_MISC_DPP 0
-#endif
-template <bool XSWZ>
-__device__ __forceinline__ uint32_t pair_swap_u32(uint32_t x) {
-  if constexpr (XSWZ && !CCV_MULTI2_MISC_DPP) return swz_quad_u32<1, 0, 3, 2>(x);
-  else return dpp_u32<0xB1>(x);
-}
-template <bool XSWZ>
-__device__ __forceinline__ float pair_swap(float x) {
-  if constexpr (XSWZ && !CCV_MULTI2_MISC_DPP) return swz_quad<1, 0, 3, 2>(x);
-  else return dpp<0xB1, float>(x);
-}
+// the pair's other lane (quad_perm [1,0,3,2]) through ds_swizzle: the argmin and the traceback keep
+// no cross-lane VALU either (with DPP there the kernel ran 34.8 instead of 37.6 Gbit/s)
+__device__ __forceinline__ uint32_t pair_swap_u32(uint32_t x) { return swz_quad_u32<1, 0, 3, 2>(x); }
+__device__ __forceinline__ float pair_swap(float x) { return swz_quad<1, 0, 3, 2>(x); }
 
 // Registers per scheduling group: a scheduling barrier after every kMulti2Group registers keeps the
 // compiler from hoisting the adds of many butterflies ahead of their mins (with 128 independent
@@ -233,10 +213,18 @@ constexpr size_t multi2_slot_bytes() {
   return (size_t)BLEN * kRegThreads * 16;   // main steps (T - (K-1) = BLEN) x 64 lanes x 16 B
 }
 
+// Ablation (timing only, output wrong): every decision store and traceback load goes to the slot's
+// first step row, so the slot traffic stays in L1 / L2 while the instruction stream is unchanged --
+// the ceiling of any slot-traffic reduction (round 5).
+#ifndef CCV_MULTI2_SLOT_ABLATE
+#define CCV_MULTI2_SLOT_ABLATE 0
+#endif
+constexpr int kMulti2StepOff(int step, int stepb) { return CCV_MULTI2_SLOT_ABLATE ? 0 : step * stepb; }
+
 #ifndef CCV_MULTI2_WAVES
 #define CCV_MULTI2_WAVES 2
 #endif
-template <CodeSpec C, int BLEN, bool XSWZ = false, int LB = 7>
+template <CodeSpec C, int BLEN, int LB = 7>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(CCV_MULTI2_WAVES)))
 void viterbi_multi2_slot(RegArgs a, int ngroups) {
   using X = Multi2<C, LB>;
@@ -320,14 +308,14 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
         const float BM[4] = {rowv.x, rowv.y, rowv.z, rowv.w};
         if constexpr (P + 1 < n) rowv = lds_read_b128<0>(rd + (swz ^ (uint32_t)((P + 1) * 16)));
         if constexpr (GROWTH) {
-          if constexpr (XSWZ && !CCV_MULTI2_MISC_DPP && X::is_lane(P)) multi2_growth_cross_swz<C, P, X>(M, BM, qb);
+          if constexpr (X::is_lane(P)) multi2_growth_cross_swz<C, P, X>(M, BM, qb);
           else multi2_growth_impl<C, P, X>(M, BM, qb, std::make_index_sequence<NR>{});
         } else {
           uint32_t D[4] = {0u, 0u, 0u, 0u};
-          if constexpr (XSWZ && X::is_lane(P)) multi2_cross_swz<C, P, X>(M, BM, qb, D);
+          if constexpr (X::is_lane(P)) multi2_cross_swz<C, P, X>(M, BM, qb, D);
           else multi2_step_impl<C, P, X>(M, BM, qb, D, std::make_index_sequence<NR>{});
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{D[0], D[1], D[2], D[3]}, slot, col,
-                                                 ((p - 1) * n + P) * STEPB, 0);
+                                                 kMulti2StepOff((p - 1) * n + P, STEPB), 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       };
@@ -345,7 +333,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     // lowest index
     static_assert(T % n == 0, "the persistent trellis ends on phase 0");
     float mn = tree_min<NR, float>(M);
-    mn = vmin(mn, pair_swap<XSWZ>(mn));   // the pair's minimum
+    mn = vmin(mn, pair_swap(mn));   // the pair's minimum
     uint32_t ne[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -358,7 +346,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     const uint32_t r0 = eq_lo ? (uint32_t)__builtin_ctzll(eq_lo) : (eq_hi ? 64u + (uint32_t)__builtin_ctzll(eq_hi) : 0xFFu);
     uint32_t idx = r0 != 0xFFu ? multi2_phys<LB>((uint32_t)q, r0) : 0xFFFFFFFFu;
     {
-      const uint32_t o = pair_swap_u32<XSWZ>(idx);
+      const uint32_t o = pair_swap_u32(idx);
       idx = o < idx ? o : idx;
     }
     const uint32_t st = mn < __builtin_inff() ? idx : 0u;   // nothing below +inf: state 0
@@ -374,7 +362,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     auto load_period = [&]<int pp>() __attribute__((always_inline)) {   // main period pp (1-based)
 #pragma unroll
       for (int P = 0; P < n; ++P)
-        dw[pp & 1][P] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, ((pp - 1) * n + P) * STEPB, kSc1);
+        dw[pp & 1][P] = __builtin_amdgcn_raw_buffer_load_b128(slot, col, kMulti2StepOff((pp - 1) * n + P, STEPB), kSc1);
     };
     auto walk_period = [&]<int pp>() __attribute__((always_inline)) {
       [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
@@ -389,7 +377,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
           const uint32_t word = (pos & 64u) ? w23 : w01;
           const uint32_t own = (word >> (pos & 31u)) & 1u;
           uint32_t m = own << qself;
-          m |= pair_swap_u32<XSWZ>(m);
+          m |= pair_swap_u32(m);
           const uint32_t d = (m >> ql) & 1u;
           if constexpr (X::is_lane(P)) {
             ql = d;

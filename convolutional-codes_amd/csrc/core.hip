@@ -28,8 +28,6 @@ bool stack_symtab_eligible(int n, int K, int T);                         // stac
 hipError_t launch_stack_symtab(uint16_t* tab, const StackArgs& a, hipStream_t s);   // stack.hip
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s);     // stack.hip
 size_t fano_order_bytes(int nblocks);                                    // stack.hip
-hipError_t launch_noise_order(const void* in, int n, int T, int nblocks, void* scratch, size_t bytes,
-                              const uint32_t** order, hipStream_t s);    // stack.hip
 hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
                              hipStream_t s);                             // stack.hip
 }
@@ -138,6 +136,20 @@ struct ccv_plan {
   DeviceBuffer sim_info, sim_out;             // ccv_simulate_device scratch (caller passed none)
   DeviceBuffer sim_frames;                    // ccv_simulate_device: K = 9 frames ahead of the wide decode
   hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
+  // ccv_plan_set_option (include/ccv.h): kernel A/B switches per plan; defaults = production paths
+  struct Options {
+    int stack_kernel = 0;            // 0 persistent rows, 1 one search per wave
+    int stack_row_lanes = 0;         // 0 auto, 8, 16
+    int stack_keys = 1;              // hard rows: packed metric / index keys where they fit
+    int stack_symtab = 1;            // rows: expected-symbol table
+    int fano_rows = -1;              // -1 auto, else ccv::kRows*
+    int fano_symtab = -1;            // -1 auto (hard input), 0 / 1
+    int fano_order = 1;              // soft: noisiest first
+    long long fano_cap = -1;         // -1 default 4000 x T, 0 one pass
+    int fano_count_moves = 0;        // diagnostics: iterations = moves
+    int channel_fused = 0;           // K = 9 soft device channel: fused multilane kernel
+    int channel_lds_decisions = -1;  // device channel K <= 7: -1 auto (BSC LDS, AWGN HBM), 0, 1
+  } opt;
 };
 
 namespace {
@@ -169,7 +181,7 @@ ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
 }
 
 // The persistent K = 9 soft kernel with a per-wave decision slot (acs_wide.hpp one lane per block for
-// the x86-idiom code, acs_multi.hpp viterbi_multi_slot four lanes per block for true parity), or
+// the x86-idiom code, acs_multi2.hpp viterbi_multi2_slot two lanes per block for true parity), or
 // nullptr: codebook block length, block-major input, decisions not exported.
 ccv::RegLaunchFn wide_kernel(const ccv_plan& p, bool export_decisions) {
   if (p.no_persistent || p.global_decisions || export_decisions || p.step_major ||
@@ -178,15 +190,14 @@ ccv::RegLaunchFn wide_kernel(const ccv_plan& p, bool export_decisions) {
   return ccv::multi_wide_launchers()[p.multi_index];
 }
 
-// The persistent kernel (acs_persist.hpp K <= 7, acs_wide.hpp / acs_multi.hpp K = 9), or nullptr:
+// The persistent kernel (acs_persist.hpp K <= 7, acs_wide.hpp / acs_multi2.hpp K = 9), or nullptr:
 // codebook block length, block-major input, decisions not exported.
 ccv::RegLaunchFn persist_kernel(const ccv_plan& p, bool export_decisions) {
   if (p.no_persistent || p.global_decisions || export_decisions || p.step_major ||
       p.d.blen != ccv::kPersistBlen)
     return nullptr;
   if (const ccv::RegLaunchFn wide = wide_kernel(p, export_decisions)) return wide;
-  if (p.multi_index >= 0)
-    return p.d.channel == CCV_SOFT ? ccv::multi_persist_launchers()[p.multi_index] : nullptr;
+  if (p.multi_index >= 0) return nullptr;   // K = 8 and other K = 9 codes: the multilane kernels
   if (p.reg_index < 0) return nullptr;
   return ccv::persist_launchers(p.d.channel == CCV_HARD)[p.reg_index];
 }
@@ -464,6 +475,38 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
   return 0;
 }
 
+int ccv_plan_set_option(ccv_plan* p, const char* name, long long value) {
+  if (!p) return fail("null plan");
+  if (!name) return fail("null option name");
+  const std::string n(name);
+  auto in = [&](long long lo, long long hi) { return value >= lo && value <= hi; };
+  auto need = [&](bool ok, const char* what) { return ok ? 0 : fail("option %s: %s", name, what); };
+  if (n == "stack_kernel" || n == "stack_row_lanes" || n == "stack_keys" || n == "stack_symtab") {
+    if (need(p->stack, "a stack-decoder plan option")) return -1;
+    if (n == "stack_kernel") { if (need(in(0, 1), "0 rows / 1 one search per wave")) return -1; p->opt.stack_kernel = (int)value; }
+    if (n == "stack_row_lanes") { if (need(value == 0 || value == 8 || value == 16, "0 (auto), 8 or 16")) return -1; p->opt.stack_row_lanes = (int)value; }
+    if (n == "stack_keys") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.stack_keys = (int)value; }
+    if (n == "stack_symtab") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.stack_symtab = (int)value; }
+    return 0;
+  }
+  if (n == "fano_rows" || n == "fano_symtab" || n == "fano_order" || n == "fano_cap" || n == "fano_count_moves") {
+    if (need(p->fano, "a Fano-decoder plan option")) return -1;
+    if (n == "fano_rows") { if (need(in(-1, 3), "-1 (auto) or 0..3")) return -1; p->opt.fano_rows = (int)value; }
+    if (n == "fano_symtab") { if (need(in(-1, 1), "-1 (auto), 0 / 1")) return -1; p->opt.fano_symtab = (int)value; }
+    if (n == "fano_order") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.fano_order = (int)value; }
+    if (n == "fano_cap") { if (need(in(-1, 0xFFFFFFFFll), "-1 (default) or moves")) return -1; p->opt.fano_cap = value; }
+    if (n == "fano_count_moves") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.fano_count_moves = (int)value; }
+    return 0;
+  }
+  if (n == "channel_fused" || n == "channel_lds_decisions") {
+    if (need(!p->stack && !p->fano, "a Viterbi plan option")) return -1;
+    if (n == "channel_fused") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.channel_fused = (int)value; }
+    if (n == "channel_lds_decisions") { if (need(in(-1, 1), "-1 (auto), 0 / 1")) return -1; p->opt.channel_lds_decisions = (int)value; }
+    return 0;
+  }
+  return fail("unknown option %s", name);
+}
+
 void ccv_plan_destroy(ccv_plan* p) {
   if (!p) return;
   if (p->svc_stream) {   // end the streaming service kernel (it polls `stop`), then wait for it
@@ -524,9 +567,7 @@ const char* ccv_plan_kernel_variant(const ccv_plan* p) {
   if (!register_path(*p)) return "generic";
   if (wide_kernel(*p, false)) {
     if (p->d.gen_mode == CCV_GEN_REF_X86) return "persistent-wide";
-    // the slot kernel's groups: 32 blocks (two lanes per block) or 16 (four lanes)
-    return ccv::multi_wide_group_blocks(p->multi_index) == ccv::kRegThreads / 2 ? "persistent-slot2"
-                                                                                 : "persistent-slot4";
+    return "persistent-slot2";   // two lanes per block (acs_multi2.hpp)
   }
   if (persist_kernel(*p, false)) return "persistent";
   if (p->multi_index >= 0) return regdec_kernel(*p, false) ? "multilane-regdec" : "multilane";
@@ -797,12 +838,11 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   a.err = d_info ? d_errors : nullptr;
   a.iterations = d_iterations;
   // two-pass schedule (fano_dev.hpp): park searches after 4000 x T moves (0.4 of the timeout), resume
-  // them in pass 2; CCV_FANO_CAP=<moves> overrides, 0 = one pass. Measured caps (tools/fano_caps.py,
+  // them in pass 2; option "fano_cap" overrides, 0 = one pass. Measured caps (tools/fano_caps.py,
   // profiles/r03_fano_caps.txt; K=15, 104 frames): 4 dB 47.3 (one pass) -> 49.4 Mbit/s at 216,000
   // moves, but 41.5 at 20,000-108,000 (half the searches park and the parking costs more than the
   // tail it saves); 6 dB 153 -> 165 at 108,000; BSC 222 -> 239 at 54,000.
-  long cap = 4000L * a.T;
-  if (const char* env = std::getenv("CCV_FANO_CAP")) cap = std::atol(env);
+  long cap = p->opt.fano_cap >= 0 ? (long)p->opt.fano_cap : 4000L * a.T;
   if (cap > 0 && nblocks > 64) {
     const size_t cap_slots = nblocks / 8 > 65536 ? nblocks / 8 : (nblocks < 65536 ? nblocks : 65536);
     const size_t mt = p->d.channel == CCV_HARD ? sizeof(int32_t) : sizeof(float);
@@ -818,28 +858,27 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
     a.park_metric = base + hdr;
     a.park_flags = reinterpret_cast<uint8_t*>(base + hdr + met);
   }
-  if (const char* env = std::getenv("CCV_FANO_COUNT_MOVES")) a.count_moves = env[0] == '1';
+  a.count_moves = p->opt.fano_count_moves;
   // the expected-symbol table: hard input only. For soft input the table load sits in each move's
   // dependent chain next to the row load, and the kernel waits on memory (PMC, round 4: wait 0.66 of
   // wave time, valu_frac 0.17): the ~25 VALU of parities are cheaper (4 dB: 49.6 -> 57.7 Mbit/s, with
-  // the candidate rows prefetched 55.7 -> 67.2, profiles/r04c/fano_ab.txt). CCV_FANO_SYMTAB=0/1
+  // the candidate rows prefetched 55.7 -> 67.2, profiles/r04c/fano_ab.txt). Option "fano_symtab"
   // overrides.
-  bool tab = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3) && p->d.channel == CCV_HARD;
-  if (const char* env = std::getenv("CCV_FANO_SYMTAB"))
-    tab = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3) && env[0] != '0';
+  const bool tab_ok = a.K <= ccv::kSymtabMaxK && (a.n == 2 || a.n == 3);
+  const bool tab = tab_ok && (p->opt.fano_symtab < 0 ? p->d.channel == CCV_HARD : p->opt.fano_symtab != 0);
   if (tab) {
     if (ensure_symtab(p, stream)) return -1;
     a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
   }
-  // soft input: hand out the noisiest blocks first (fano_dev.hpp, fano_score); CCV_FANO_ORDER=0 off
-  bool order = p->d.channel == CCV_SOFT && (a.n == 2 || a.n == 3) && nblocks > 64;
-  if (const char* env = std::getenv("CCV_FANO_ORDER")) order = order && env[0] != '0';
+  // soft input: hand out the noisiest blocks first (fano_dev.hpp, fano_score); option "fano_order" 0 off
+  const bool order = p->opt.fano_order && p->d.channel == CCV_SOFT && (a.n == 2 || a.n == 3) && nblocks > 64;
   if (order) {
     const size_t need = ccv::fano_order_bytes(a.nblocks);
     if (p->order.grow(need, stream)) return -1;
     HIP_TRY(ccv::launch_fano_order(a, p->order.ptr, p->order.bytes, &a.order, stream));
   }
-  const bool debug = std::getenv("CCV_FANO_DEBUG") != nullptr;
+  a.rows_mode = p->opt.fano_rows;
+  const bool debug = std::getenv("CCV_DEBUG") != nullptr;
   if (debug)   // diagnostics: synchronous, prints lane utilisation (both passes together)
     a.stats = reinterpret_cast<unsigned long long*>(ctr + 4);
   HIP_TRY(ccv::launch_fano(a, p->d.channel == CCV_HARD, stream));
@@ -891,25 +930,17 @@ int ccv_stack_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, const
   a.err = d_info ? d_errors : nullptr;
   a.status = d_status;
   hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
-  if (ccv::stack_rows_eligible(a.n, a.K, a.T)) {   // persistent rows pull blocks from a counter
+  a.opt_row_lanes = p->opt.stack_row_lanes;
+  a.opt_keys = p->opt.stack_keys;
+  // persistent rows pull blocks from a counter (the noisiest-first order of the Fano decoder was
+  // measured 3 % slower here, profiles/r04x/, and removed in round 5)
+  if (p->opt.stack_kernel == 0 && ccv::stack_rows_eligible(a.n, a.K, a.T)) {
     if (p->counter.grow(sizeof(unsigned int), stream)) return -1;
     HIP_TRY(hipMemsetAsync(p->counter.ptr, 0, sizeof(unsigned int), stream));
     a.next_block = static_cast<unsigned int*>(p->counter.ptr);
-    if (ccv::stack_symtab_eligible(a.n, a.K, a.T)) {
+    if (p->opt.stack_symtab && ccv::stack_symtab_eligible(a.n, a.K, a.T)) {
       if (ensure_symtab(p, stream)) return -1;
       a.symtab = static_cast<const uint16_t*>(p->symtab.ptr);
-    }
-    // CCV_STACK_ORDER=1 (A/B, soft input): noisiest blocks first, the Fano decoder's order
-    // (stack.hip launch_noise_order). Measured 3 % SLOWER than the natural order at 4 and 16 frames
-    // (profiles/r04x/), so off by default.
-    bool order = false;
-    if (const char* env = std::getenv("CCV_STACK_ORDER"))
-      order = env[0] == '1' && p->d.channel == CCV_SOFT && (a.n == 2 || a.n == 3) && nblocks > 64;
-    if (order) {
-      const size_t need = ccv::fano_order_bytes(a.nblocks);
-      if (p->order.grow(need, stream)) return -1;
-      HIP_TRY(ccv::launch_noise_order(a.in, a.n, a.T, a.nblocks, p->order.ptr, p->order.bytes, &a.order,
-                                      stream));
     }
   }
   HIP_TRY(ccv::launch_stack(a, p->d.channel == CCV_HARD, stream));
@@ -923,6 +954,8 @@ static int simulate_frames_only(ccv_plan* p, uint64_t seed, uint64_t first_block
                                 void* d_channel, void* stream_v) {
   const bool hard = p->d.channel == CCV_HARD;
   if (!d_channel) return fail("CCV_CHANNEL_FRAMES_ONLY needs d_channel");
+  // the frames are written block-major, which a step-major plan would decode as scrambled input
+  if (p->step_major) return fail("CCV_CHANNEL_FRAMES_ONLY writes block-major frames: not for a step-major plan");
   if (p->d.n > 3) return fail("frames-only channel: n = %d (n <= 3)", p->d.n);
   if (hard && !(channel_param >= 0.0 && channel_param <= 1000000.0))
     return fail("BSC p_ppm must be in [0, 1e6]");
@@ -987,7 +1020,7 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   // lane per block, acs_wide.hpp; true parity: acs_multi.hpp) with the fused error count -- the
   // multilane channel kernel draws every block's channel once per lane of its four-lane group
   const bool frames_path = !hard && p->multi_index >= 0 && persist_kernel(*p, false) != nullptr &&
-                           std::getenv("CCV_CHANNEL_FUSED") == nullptr;
+                           !p->opt.channel_fused;
   if (!frames_path && p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
   ccv::ChanArgs a{};
   a.r.in = nullptr;
@@ -1011,9 +1044,8 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   // Decisions in LDS (viterbi_channel_lds) for BSC, in HBM scratch for AWGN: the 20 KiB column per
   // wave caps a CU at 8 waves; the BSC kernel gains more from the saved decision traffic (108.6 vs
   // 96.6 Gbit/s at K=7), the double-precision AWGN kernel loses more occupancy than it saves (60.3
-  // vs 62.5). CCV_CHANNEL_LDS_DECISIONS=1 / =0 forces either (A/B).
-  const char* lds_env = std::getenv("CCV_CHANNEL_LDS_DECISIONS");
-  const bool lds_dec = lds_env && lds_env[0] ? lds_env[0] == '1' : hard;
+  // vs 62.5). Option "channel_lds_decisions" 1 / 0 forces either (A/B).
+  const bool lds_dec = p->opt.channel_lds_decisions < 0 ? hard : p->opt.channel_lds_decisions != 0;
   a.global_decisions = (p->global_decisions || !lds_dec) ? 1 : 0;
   if (frames_path) {
     void* frames = d_channel;

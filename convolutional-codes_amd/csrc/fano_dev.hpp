@@ -58,9 +58,9 @@ struct FanoArgs {
   const uint8_t* info;       // optional: count bit errors
   unsigned long long* err;
   uint32_t* iterations;      // optional [nb]: search iterations used (timeout = 10000 * T)
-  int count_moves;           // diagnostics (CCV_FANO_COUNT_MOVES=1): `iterations` gets the number of
+  int count_moves;           // diagnostics (option "fano_count_moves"): `iterations` gets the number of
                              // moves (forward, back, threshold relaxations) instead
-  unsigned long long* stats; // diagnostics (CCV_FANO_DEBUG): [0] sum over waves of loop passes,
+  unsigned long long* stats; // diagnostics (CCV_DEBUG): [0] sum over waves of loop passes,
                              // [1] sum over lanes of passes in which the lane had a search to advance
   const uint16_t* symtab;    // TAB: [2^(K-1)] expected symbols (stack_symtab_init), K <= kSymtabMaxK
   const uint32_t* order;     // optional [nb]: the queue hands out block order[q] (noisiest first)
@@ -73,6 +73,7 @@ struct FanoArgs {
   uint32_t* park_hdr;        // [nb][kFanoParkWords]: block, cur, frontier, state, metrics, flags
   void* park_metric;         // [nb][T + 1] path metrics of the nodes 0..frontier
   uint8_t* park_flags;       // [nb][T + 1] sel | dec << 1 of the nodes 0..frontier
+  int rows_mode;             // host only (ccv_plan_set_option "fano_rows"): -1 auto, else kRows*
 };
 
 constexpr int kFanoParkWords = 12;
@@ -109,7 +110,11 @@ constexpr int kFanoThreads = 64;
 //     cur + 1) and the lane keeps its own node's row in registers, so the load latency overlaps the
 //     pass instead of following it (hard input or rate 1/2: a row is a byte or a float4).
 //   kRowsLds: as kRowsGlobal, the block's rows copied into LDS when the lane takes the block.
-constexpr int kRowsDirect = 0, kRowsGlobal = 2, kRowsLds = 1;
+//   kRowsWindow: the rows of cur - 1, cur and cur + 1 stay in registers; a move shifts the window
+//     and issues ONE load, the row beyond its new edge, which the lane first reads at the end of its
+//     NEXT pass -- a whole pass of latency hiding instead of part of one, and one load per pass
+//     instead of two (round 5; rate 1/2 soft input).
+constexpr int kRowsDirect = 0, kRowsGlobal = 2, kRowsLds = 1, kRowsWindow = 3;
 template <bool HARD, int NP>
 struct FanoRow;
 template <int NP>
@@ -146,6 +151,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   using ST = typename std::conditional<W32, uint32_t, uint64_t>::type;
   static_assert(RM == kRowsDirect || HARD || NP == 2, "rows of received symbols are a byte or a float4");
   constexpr bool ROWS = RM != kRowsDirect;
+  constexpr bool WIN = RM == kRowsWindow;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const int T = a.T, K = a.K, n = a.n;
@@ -236,6 +242,10 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   bool inback = false, moved = false;
   uint32_t moves = 0, spass = 0;
   FanoRow<HARD, NP> row0{};   // received row of node cur
+  // WIN: rows of cur - 1 (rwa) and cur + 1 (rwb), except that the side of the last move is still in
+  // flight in rwn (pdir = +1: rwn is cur + 1's row, -1: cur - 1's, 0: no load pending)
+  FanoRow<HARD, NP> rwa{}, rwb{}, rwn{};
+  int pdir = 0;
   auto as_bits = [](MT v) -> uint32_t {
     if constexpr (HARD) return (uint32_t)v;
     else return __float_as_uint(v);
@@ -307,6 +317,11 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     moves = h[11];
     spass = 0;
     if constexpr (ROWS) row0 = row_at(cur);
+    if constexpr (WIN) {
+      rwa = row_at(cur > 0 ? cur - 1 : 0);
+      rwb = row_at(cur + 1 < T ? cur + 1 : T - 1);
+      pdir = 0;
+    }
   };
   // start a search (:108-124 reset, then the root's branch metrics)
   auto start = [&]() {
@@ -319,6 +334,11 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     load_rows();
     spass = 0;
     if constexpr (ROWS) row0 = row_at(0);
+    if constexpr (WIN) {
+      rwa = row0;
+      rwb = row_at(1 < T ? 1 : 0);
+      pdir = 0;
+    }
     metric[lane] = (MT)0;
     cur = 0;
     frontier = 0;
@@ -384,7 +404,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     const uint32_t fprev = flags[cm * kFanoThreads + lane];
     const uint32_t fold = flags[(cur >= K ? cur - K : 0) * kFanoThreads + lane];
     FanoRow<HARD, NP> rowm{}, rowp{};
-    if constexpr (ROWS) {
+    if constexpr (ROWS && !WIN) {
       rowm = row_at(cm);
       rowp = row_at(cur + 1 < T ? cur + 1 : T - 1);
     }
@@ -429,7 +449,24 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       continue;
     }
     metric[(fwd ? ncur : T) * kFanoThreads + lane] = ms;
-    if constexpr (ROWS) row0.pick(fwd, rowp, bstep, rowm);
+    if constexpr (WIN) {
+      // the previous pass's load lands here, one pass after it was issued
+      FanoRow<HARD, NP> ea = rwa, eb = rwb;
+      ea.pick(pdir < 0, rwn, false, rwn);
+      eb.pick(pdir > 0, rwn, false, rwn);
+      const FanoRow<HARD, NP> old0 = row0;
+      row0.pick(fwd, eb, bstep, ea);
+      rwa = ea;
+      rwa.pick(fwd, old0, false, old0);
+      rwb = eb;
+      rwb.pick(bstep, old0, false, old0);
+      // the row beyond the new edge (clamped into the block: never read when clamped)
+      const int edge = fwd ? (ncur + 1 < T ? ncur + 1 : T - 1) : (ncur > 0 ? ncur - 1 : 0);
+      rwn = row_at(edge);
+      pdir = fwd ? 1 : (bstep ? -1 : 0);
+    } else if constexpr (ROWS) {
+      row0.pick(fwd, rowp, bstep, rowm);
+    }
     MT n0, n1;
     uint32_t sw;
     node_metrics(rx, ncur, st, row0, n0, n1, sw);

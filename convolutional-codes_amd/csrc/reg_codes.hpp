@@ -61,14 +61,10 @@ const RegLaunchFn* multi_launchers(bool hard);   // [kNumMultiCodes], reg_multi.
 // T <= multi_regdec_max_steps(K) and no decision export (reg_multi.hip)
 const RegLaunchFn* multi_regdec_launchers(bool hard);
 int multi_regdec_max_steps(int K);
-// [kNumMultiCodes] persistent soft kernel (acs_multi.hpp viterbi_multi_persist; int argument =
-// groups of 64 / 2^(K-7) blocks), nullptr where a code has none (K = 9, r = 1/2 only); valid for
-// blen == kPersistBlen, block-major input, no decision export (reg_multi.hip)
-const RegLaunchFn* multi_persist_launchers();
 // [kNumMultiCodes] persistent soft kernels whose decisions go through a per-wave scratch slot,
 // nullptr where a code has none: the K = 9 x86-idiom code runs one lane per block (acs_wide.hpp
-// viterbi_wide_persist: 156 distinct metrics fit one lane's VGPRs), the true-parity K = 9 code four
-// lanes per block with its main periods as a loop (acs_multi.hpp viterbi_multi_slot). int argument =
+// viterbi_wide_persist: 156 distinct metrics fit one lane's VGPRs), the true-parity K = 9 code two
+// lanes per block with its main periods as a loop (acs_multi2.hpp viterbi_multi2_slot). int argument =
 // groups of multi_wide_group_blocks(index) blocks; RegArgs::dec = one scratch slot of
 // multi_wide_slot_bytes(index) per resident wave of the grid. Valid for blen == kPersistBlen,
 // block-major input, no decision export (reg_multi.hip)

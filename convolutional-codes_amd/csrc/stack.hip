@@ -35,9 +35,7 @@ template <bool HARD, int NP, bool TAB, int RL, bool KEY = false>
 static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
   constexpr int kStackRows = kStackDepth / RL;   // searches per wave
   const void* fn = reinterpret_cast<const void*>(&stack_decode_rows<HARD, NP, TAB, RL, KEY>);
-  size_t lds = (size_t)kStackRows * stack_rows_row_bytes(a.T, HARD ? 1 : 1 << NP, HARD);
-  if (const char* env = std::getenv("CCV_STACK_EXTRA_LDS"))   // occupancy studies: unused LDS per wave
-    lds += (size_t)std::atol(env);
+  const size_t lds = (size_t)kStackRows * stack_rows_row_bytes(a.T, HARD ? 1 : 1 << NP, HARD);
   int dev = 0, cus = 0, per_cu = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -46,7 +44,7 @@ static hipError_t launch_rows(const StackArgs& a, hipStream_t s) {
   const long resident = (long)(cus > 0 ? cus : 1) * (per_cu > 0 ? per_cu : 1);
   const long waves_needed = ((long)a.nblocks + kStackRows - 1) / kStackRows;
   const int grid = (int)(waves_needed < resident ? waves_needed : resident);
-  if (std::getenv("CCV_STACK_DEBUG"))
+  if (std::getenv("CCV_DEBUG"))
     std::fprintf(stderr, "stack rows: %d lanes per search, table %d, keys %d, lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n",
                  RL, (int)TAB, (int)KEY, lds, per_cu, cus, grid);
   hipLaunchKernelGGL((stack_decode_rows<HARD, NP, TAB, RL, KEY>), dim3(grid), dim3(kStackDepth), lds, s, a);
@@ -59,15 +57,11 @@ static hipError_t launch_rows_t(const StackArgs& a, hipStream_t s) {
   // per scan. Lanes per search: 16, except hard input without keys: 8 (8 entries per lane, 8 searches
   // per wave -- fewer DPP steps, but twice the LDS per wave, which for soft input caps a CU at 9 waves).
   // Measured (profiles/r02c_stack_ab.txt): soft 16 lanes 546 vs 8 lanes 519 Mbit/s; hard keyed
-  // 16 lanes 1275, 8 lanes 1259, unkeyed 8 lanes 1104-1152, 16 lanes 1073. CCV_STACK_ROWL=8/16 and
-  // CCV_STACK_KEYS=0 override.
+  // 16 lanes 1275, 8 lanes 1259, unkeyed 8 lanes 1104-1152, 16 lanes 1073. The plan options
+  // "stack_row_lanes" and "stack_keys" override.
   bool keyed = false;
-  if constexpr (HARD) {
-    keyed = a.symtab != nullptr && stack_rows_keyed(a.T, a.n, a.bm0, a.bm1);
-    if (const char* env = std::getenv("CCV_STACK_KEYS")) keyed = keyed && env[0] != '0';
-  }
-  int rl = HARD && !keyed ? 8 : 16;
-  if (const char* env = std::getenv("CCV_STACK_ROWL")) rl = std::atoi(env);
+  if constexpr (HARD) keyed = a.opt_keys && a.symtab != nullptr && stack_rows_keyed(a.T, a.n, a.bm0, a.bm1);
+  const int rl = a.opt_row_lanes ? a.opt_row_lanes : (HARD && !keyed ? 8 : 16);
   if (keyed) {
     if (rl == 8) return launch_rows<HARD, NP, true, 8, HARD>(a, s);
     return launch_rows<HARD, NP, true, 16, HARD>(a, s);
@@ -76,11 +70,7 @@ static hipError_t launch_rows_t(const StackArgs& a, hipStream_t s) {
   return a.symtab ? launch_rows<HARD, NP, true, 16>(a, s) : launch_rows<HARD, NP, false, 16>(a, s);
 }
 
-bool stack_symtab_eligible(int n, int K, int T) {
-  if (const char* env = std::getenv("CCV_STACK_SYMTAB"))   // A/B: 0 = parities per iteration
-    if (env[0] == '0') return false;
-  return stack_rows_eligible(n, K, T) && K <= kSymtabMaxK;
-}
+bool stack_symtab_eligible(int n, int K, int T) { return stack_rows_eligible(n, K, T) && K <= kSymtabMaxK; }
 
 hipError_t launch_stack_symtab(uint16_t* tab, const StackArgs& a, hipStream_t s) {
   const unsigned S = 1u << (a.K - 1);
@@ -90,11 +80,7 @@ hipError_t launch_stack_symtab(uint16_t* tab, const StackArgs& a, hipStream_t s)
   return hipGetLastError();
 }
 
-bool stack_rows_eligible(int n, int K, int T) {
-  if (const char* env = std::getenv("CCV_STACK_WAVE"))   // A/B: one search per wave
-    if (env[0] == '1') return false;
-  return K <= 32 && (n == 2 || n == 3) && T <= kRowsMaxT;
-}
+bool stack_rows_eligible(int n, int K, int T) { return K <= 32 && (n == 2 || n == 3) && T <= kRowsMaxT; }
 
 hipError_t launch_stack(const StackArgs& a, bool hard, hipStream_t s) {
   if (stack_rows_eligible(a.n, a.K, a.T) && a.next_block != nullptr) {
@@ -153,7 +139,7 @@ static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
   const int resident = (cus > 0 ? cus : 1) * (per_cu > 0 ? per_cu : 1);
   const int waves_needed = (a.nblocks + kFanoThreads - 1) / kFanoThreads;
   const int grid = waves_needed < resident ? waves_needed : resident;
-  if (std::getenv("CCV_FANO_DEBUG"))
+  if (std::getenv("CCV_DEBUG"))
     std::fprintf(stderr, "fano: lds %zu B/wave, %d waves/CU x %d CUs, grid %d\n", lds, per_cu, cus, grid);
   hipLaunchKernelGGL((fano_decode<HARD, NP, W32, RM>), dim3(grid), dim3(kFanoThreads), lds, s, a);
   return hipGetLastError();
@@ -162,6 +148,7 @@ static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
 template <bool HARD>
 static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream_t s) {
   if (a.K <= 32 && a.n == 2) {
+    if (rm == kRowsWindow) return launch_fano_v<HARD, 2, true, kRowsWindow>(a, lds, s);
     if (rm == kRowsLds) return launch_fano_v<HARD, 2, true, kRowsLds>(a, lds, s);
     if (rm == kRowsGlobal) return launch_fano_v<HARD, 2, true, kRowsGlobal>(a, lds, s);
     return launch_fano_v<HARD, 2, true, kRowsDirect>(a, lds, s);
@@ -182,16 +169,17 @@ static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream
 // ~10 % slower (profiles/r01_fano.txt), but the round-3 one-loop kernel waits on memory (PMC, round 4:
 // wait 0.66, valu_frac 0.17) and the prefetch now wins: 4 dB 49.6 -> 55.7 Mbit/s, 67.2 with the
 // parities computed instead of the table load (profiles/r04c/fano_ab.txt). Soft K=15 rows in LDS
-// (16 B per node) cut the chip from 9 to 2 waves per CU and run 4x slower. CCV_FANO_ROWS=0/1/2
-// overrides.
+// (16 B per node) cut the chip from 9 to 2 waves per CU and run 4x slower. The plan option
+// "fano_rows" (FanoArgs::rows_mode) overrides.
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
   const size_t node_bytes = ((size_t)(a.T + 1) * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1) + 15) & ~(size_t)15;
   const size_t row_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : 16);
   const bool rowable = hard || (a.n == 2 && a.K <= 32);
   int rm = hard ? kRowsLds : (rowable ? kRowsGlobal : kRowsDirect);
-  if (const char* env = std::getenv("CCV_FANO_ROWS")) rm = rowable ? env[0] - '0' : kRowsDirect;
+  if (a.rows_mode >= 0) rm = rowable ? a.rows_mode : kRowsDirect;
   if (rm == kRowsLds && node_bytes + row_bytes > 80 * 1024) rm = kRowsGlobal;
-  if (rm < 0 || rm > 2) rm = kRowsDirect;
+  if (rm == kRowsWindow && !(a.n == 2 && a.K <= 32)) rm = kRowsGlobal;
+  if (rm < 0 || rm > 3) rm = kRowsDirect;
   const size_t lds = node_bytes + (rm == kRowsLds ? row_bytes : 0);
   return hard ? launch_fano_h<true>(a, rm, lds, s) : launch_fano_h<false>(a, rm, lds, s);
 }
@@ -206,7 +194,7 @@ size_t fano_order_bytes(int nblocks) {
   return 16 * (size_t)nblocks + tmp + 256;
 }
 
-hipError_t launch_noise_order(const void* in_v, int n_out, int T, int nblocks, void* scratch, size_t bytes,
+static hipError_t noise_order(const void* in_v, int n_out, int T, int nblocks, void* scratch, size_t bytes,
                               const uint32_t** order, hipStream_t s) {
   const size_t n = (size_t)nblocks;
   float* k_in = static_cast<float*>(scratch);
@@ -230,7 +218,7 @@ hipError_t launch_noise_order(const void* in_v, int n_out, int T, int nblocks, v
 
 hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
                              hipStream_t s) {
-  return launch_noise_order(a.in, a.n, a.T, a.nblocks, scratch, bytes, order, s);
+  return noise_order(a.in, a.n, a.T, a.nblocks, scratch, bytes, order, s);
 }
 
 }  // namespace ccv

@@ -48,7 +48,8 @@ struct StackArgs {
   int32_t* status;         // optional [nb]: 0 ok, 1 = the reference would read past its buffers
   unsigned int* next_block;  // stack_decode_rows: work counter, zero before the launch
   const uint16_t* symtab;    // stack_decode_rows, K <= kSymtabMaxK: [2^(K-1)] expected symbols
-  const uint32_t* order;     // stack_decode_rows, optional [nb]: the counter hands out block order[q]
+  int opt_row_lanes;         // host only (ccv_plan_set_option): 0 auto, 8, 16 lanes per search
+  int opt_keys;              // host only: packed metric / index keys for hard input where they fit
 };
 
 constexpr int kStackDepth = 64;   // stack-decoder.c:12 == wave64
@@ -485,14 +486,10 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
   };
   const uint32_t esym_root = symbols_of(0);
 
-  // the next block: the work counter, through the noisiest-first order when there is one (the
-  // long searches start first instead of forming the launch's tail; outputs stay per block index)
+  // the next block from the work counter
   auto fetch = [&]() -> int {
     uint32_t b = 0;
-    if (l == 0) {
-      b = atomicAdd(a.next_block, 1u);
-      if (a.order != nullptr && b < (uint32_t)nb) b = a.order[b];
-    }
+    if (l == 0) b = atomicAdd(a.next_block, 1u);
     return __shfl((int)b, rbase, 64);
   };
   // stage a block's symbols and the root entry; the row's LDS is private to its 16 lanes

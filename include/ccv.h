@@ -90,8 +90,8 @@ int ccv_plan_trellis(const ccv_plan* plan, uint8_t* exp);
 int ccv_plan_decision_storage(const ccv_plan* plan);
 
 /* Name of the kernel a ccv_decode_device call without decision export runs: "persistent",
- * "persistent-wide" (K = 9, one lane per block), "persistent-slot2" / "persistent-slot4" (K = 9 true
- * parity, two / four lanes per block), "register-regdec", "register", "multilane-regdec", "multilane",
+ * "persistent-wide" (K = 9, one lane per block), "persistent-slot2" (K = 9 true parity, two lanes
+ * per block), "register-regdec", "register", "multilane-regdec", "multilane",
  * "generic", "stack" or "fano". */
 const char* ccv_plan_kernel_variant(const ccv_plan* plan);
 
@@ -130,7 +130,8 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
 #define CCV_CHANNEL_HARD_DEMAP 1u   /* AWGN: common/hard-demapper.c instead of common/demapper.c */
 /* Frames only, no decode: info bytes into d_info (or plan scratch) and the decoder input into d_channel
  * (required), same draws as above, for ANY plan -- Viterbi, stack or Fano, n <= 3, K <= 64. d_out,
- * d_path_metric and d_errors are ignored. The device sweeps of the sequential decoders use it. */
+ * d_path_metric and d_errors are ignored. The frames are block-major ([nb][T][2^n] / [nb][T]): a
+ * CCV_FLAG_STEP_MAJOR plan is rejected (-1). The device sweeps of the sequential decoders use it. */
 #define CCV_CHANNEL_FRAMES_ONLY 2u
 int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,
@@ -181,6 +182,24 @@ int ccv_stack_decode_host(ccv_plan* plan, const void* in, size_t nblocks, const 
  * meanwhile. CCV_HOST_LATENCY=1 launches one kernel per call instead; ccv_plan_destroy stops it. */
 int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out,
                     int32_t* path_metric);
+
+/* Per-plan kernel options: A/B switches for measurements and tests; the defaults are the measured-
+ * best paths. Takes effect from the plan's next decode. Returns 0, or -1 for an unknown
+ * name, a value out of range or an option of another decoder.
+ *   stack plans:  "stack_kernel"     0 persistent rows (default), 1 one search per wave
+ *                 "stack_row_lanes"  0 auto (16; 8 for hard input without keys), 8, 16
+ *                 "stack_keys"       1 packed metric / index keys for hard input where they fit (default), 0
+ *                 "stack_symtab"     1 expected-symbol table (default), 0 parities per iteration
+ *   Fano plans:   "fano_rows"        -1 auto (default: 1 hard, 2 soft r = 1/2), 0 read after the move,
+ *                                    1 LDS, 2 both candidates prefetched, 3 register window
+ *                 "fano_symtab"      -1 auto (table for hard input), 0, 1
+ *                 "fano_order"       1 noisiest blocks first for soft input (default), 0 natural order
+ *                 "fano_cap"         -1 default (4000 x T moves), 0 one pass, else moves before parking
+ *                 "fano_count_moves" 1: d_iterations gets moves instead of timeout ticks (diagnostics)
+ *   Viterbi plans (on-device channel):
+ *                 "channel_fused"    1: K = 9 soft codes use the fused multilane channel kernel
+ *                 "channel_lds_decisions"  -1 auto (BSC LDS, AWGN HBM), 0 HBM, 1 LDS (K <= 7) */
+int ccv_plan_set_option(ccv_plan* plan, const char* name, long long value);
 
 /* Achievable-HBM probe for the roofline (bench.py): one streaming pass over `bytes` (a multiple of
  * 16, 16-byte aligned buffers) with global_load_dwordx4 -- mode 0 copies src to dst

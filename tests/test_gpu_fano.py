@@ -98,23 +98,24 @@ def test_fano_timeouts_iterations_and_error_count(torch_cuda):
     assert (it < 10000 * c.steps).any()
 
 
-@pytest.mark.parametrize("table", ["1", "0"])
-def test_fano_queue_order_and_symbol_table_change_nothing(torch_cuda, monkeypatch, table):
-    """The noisiest-first queue order (soft input) and the expected-symbol table only change the
-    schedule and where the symbols come from: outputs, error count and every block's search length
-    equal the natural-order run and the oracle (K=15, 2 dB: long searches and timeouts)."""
+@pytest.mark.parametrize("rows", [-1, 0, 2, 3], ids=["rows_auto", "rows_direct", "rows_pair", "rows_window"])
+@pytest.mark.parametrize("table", [1, 0])
+def test_fano_queue_order_and_symbol_table_change_nothing(torch_cuda, table, rows):
+    """The noisiest-first queue order (soft input), the expected-symbol table and the received-row
+    access (after the move, both candidates prefetched, the register window of round 5) only change
+    the schedule and where the symbols come from: outputs, error count and every block's search
+    length equal the natural-order run and the oracle (K=15, 2 dB: long searches and timeouts)."""
     torch = torch_cuda
-    monkeypatch.setenv("CCV_FANO_SYMTAB", table)
     c = K15
     nb = 700
     info, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 11)
     ref = O.fano_soft(_ocode(c), c.fano_metric_weight, rx)
-    plan = FanoPlan(c, SOFT)
+    plan = FanoPlan(c, SOFT).set_option("fano_symtab", table).set_option("fano_rows", rows)
     d_rx = torch.from_numpy(rx).cuda()
     d_info = torch.from_numpy(info).cuda()
     runs = []
-    for order in ("1", "0"):
-        monkeypatch.setenv("CCV_FANO_ORDER", order)
+    for order in (1, 0):
+        plan.set_option("fano_order", order)
         d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
         d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
         d_it = torch.zeros(nb, dtype=torch.int32, device="cuda")
@@ -144,22 +145,20 @@ def _two_pass_case(channel):
     return _TWO_PASS[channel]
 
 
+@pytest.mark.parametrize("rows", [-1, 3], ids=["rows_auto", "rows_window"])
 @pytest.mark.parametrize("channel", [SOFT, HARD], ids=["soft", "hard"])
-@pytest.mark.parametrize("cap", ["0", "7", "300", "default"])
-def test_fano_two_pass_park_and_resume_is_exact(torch_cuda, monkeypatch, channel, cap):
-    """The two-pass schedule (fano_dev.hpp): searches parked after CCV_FANO_CAP moves and resumed in
+@pytest.mark.parametrize("cap", [0, 7, 300, -1], ids=["cap0", "cap7", "cap300", "default"])
+def test_fano_two_pass_park_and_resume_is_exact(torch_cuda, channel, cap, rows):
+    """The two-pass schedule (fano_dev.hpp): searches parked after `fano_cap` moves and resumed in
     pass 2 -- after 7 moves nearly every search parks mid-flight (forward runs, look-backs, threshold
     relaxations), after 300 only the long ones -- give the one-pass (cap 0) outputs, path metrics,
-    error count and per-block search lengths, and the oracle's outputs (K=15, timeouts included)."""
+    error count and per-block search lengths, and the oracle's outputs (K=15, timeouts included); with
+    the default rows and the register row window (a parked search restores its window)."""
     torch = torch_cuda
-    if cap == "default":
-        monkeypatch.delenv("CCV_FANO_CAP", raising=False)
-    else:
-        monkeypatch.setenv("CCV_FANO_CAP", cap)
     c = K15
     nb = 900
     info, rx, ref, ref_pm = _two_pass_case(channel)
-    plan = FanoPlan(c, channel)
+    plan = FanoPlan(c, channel).set_option("fano_cap", cap).set_option("fano_rows", rows)
     d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
     d_pm = torch.zeros(nb, dtype=torch.int32, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -178,7 +177,7 @@ def test_fano_two_pass_park_and_resume_is_exact(torch_cuda, monkeypatch, channel
     if channel == SOFT:
         assert (it == 10000 * c.steps).any()
     # the search lengths equal the one-pass run's
-    monkeypatch.setenv("CCV_FANO_CAP", "0")
+    plan.set_option("fano_cap", 0)
     d_it0 = torch.zeros(nb, dtype=torch.int32, device="cuda")
     plan.decode_fano_device(torch.from_numpy(rx).cuda(), nb, d_out,
                             d_path_metric=d_pm if channel == HARD else None, d_iterations=d_it0)

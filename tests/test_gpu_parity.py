@@ -15,7 +15,7 @@ import oracle_ctypes as O
 from ccviterbi import (CODEBOOK, GEN_REF_X86, GEN_TRUE_PARITY, HARD, K7, K8, K9, SOFT, Code,
                        HardDecoder, Plan, SoftDecoder, channel as ch)
 from ccviterbi import sim
-from ccviterbi.decoder import FLAG_GENERIC, FLAG_GLOBAL_DECISIONS, FLAG_NO_PERSISTENT
+from ccviterbi.decoder import FLAG_GENERIC, FLAG_GLOBAL_DECISIONS, FLAG_NO_PERSISTENT, FLAG_STEP_MAJOR
 from conftest import golden_manifest
 
 pytestmark = pytest.mark.gpu
@@ -92,7 +92,7 @@ def test_register_kernel_selected_for_benchmark_codes():
     # K = 8, 9 (multilane kernel): register-resident up to T = 48 (K9) / 49 (K8), soft and hard
     for c in (K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
         # the K = 9 x86-idiom soft code runs one lane per block with a per-wave decision slot
-        # (the true-parity K = 9 code four lanes per block with a slot too, viterbi_multi_slot)
+        # (the true-parity K = 9 code two lanes per block with a slot too, viterbi_multi2_slot)
         soft = "slot" if c.K == 9 else "registers"
         assert Plan(c, SOFT).decisions == soft and Plan(c, HARD).decisions == "registers"
         assert Plan(c, SOFT, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
@@ -452,38 +452,17 @@ def test_k9_wide_kernel(torch_cuda, nb, gen):
     assert np.array_equal(out[sample], O.viterbi_soft(_ocode(c), rx[sample]))
 
 
-_LANES_SCRIPT = r'''
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-from ccviterbi import K9, SOFT, GEN_TRUE_PARITY, Plan, channel as ch
-c = K9.with_(gen_mode=GEN_TRUE_PARITY)
-nb = int(sys.argv[2])
-_, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 515)
-plan = Plan(c, SOFT)
-print(plan.variant)
-np.save(sys.argv[3], plan.decode_host(rx))
-'''
 
 
-@pytest.mark.parametrize("lanes,variant", [("4", "persistent-slot4"), ("2", "persistent-slot2")])
-def test_k9_true_lane_variants(torch_cuda, tmp_path, lanes, variant):
-    """The true-parity K = 9 kernel's A/B forms (CCV_K9_TRUE_LANES, read once per process, so each
-    runs in a child process): four lanes per block (acs_multi.hpp) and two (acs_multi2.hpp, the
-    default) decode a ragged multi-group batch identically to the oracle."""
-    import os
-    import subprocess
-    import sys
-    from conftest import REPO
-    nb = 3 * 2048 + 77
-    out_path = str(tmp_path / "out.npy")
-    env = dict(os.environ, CCV_K9_TRUE_LANES=lanes)
-    r = subprocess.run([sys.executable, "-c", _LANES_SCRIPT, os.path.join(REPO, "convolutional-codes_amd"),
-                        str(nb), out_path], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert r.stdout.split()[-1] == variant
+def test_k9_true_two_lane_kernel_ragged_groups(torch_cuda):
+    """The true-parity K = 9 kernel (two lanes per block, acs_multi2.hpp) decodes a ragged batch of
+    several rounds of 32-block groups over the resident waves identically to the oracle."""
     c = K9.with_(gen_mode=GEN_TRUE_PARITY)
+    plan = Plan(c, SOFT)
+    assert plan.variant == "persistent-slot2"
+    nb = 3 * 2048 + 77
     _, rx = ch.awgn_blocks(c, nb, ch.noise_scaling(2.0), 515)
-    assert np.array_equal(np.load(out_path), O.viterbi_soft(_ocode(c), rx))
+    assert np.array_equal(plan.decode_host(rx), O.viterbi_soft(_ocode(c), rx))
 
 
 def test_multilane_error_count_and_no_decision_export(torch_cuda):
@@ -841,6 +820,21 @@ def test_device_channel_bsc_bit_exact(torch_cuda, name, c):
         assert err == ch.count_bit_errors(c, info, out)
 
 
+# The device channel's double log / sqrt / sincos (channel_math.hpp) against glibc's: the host
+# checker with the hardware approximations emulated measures 0 - 2.2e-8 of the fp32 samples differing
+# (tools/chanmath_check.cpp, profiles/r04_chanmath_check.txt), i.e. ~0.001 expected at these test
+# sizes. Allow 2, so a device-only precision loss (v_rsq_f64 / v_rcp_f64 less exact than emulated)
+# fails here instead of hiding under a 0.1 % gate.
+MAX_CHANNEL_DIFFS = 2
+
+
+def _assert_samples_match(rx, h_rx, hard_demap=False):
+    diff = np.any(rx != h_rx, axis=2) if hard_demap else (rx != h_rx)
+    assert int(np.count_nonzero(diff)) <= MAX_CHANNEL_DIFFS, (int(np.count_nonzero(diff)), diff.size)
+    if not hard_demap:
+        assert np.allclose(rx, h_rx, rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("name,c", CHANNEL_CODES, ids=[x[0] for x in CHANNEL_CODES])
 def test_device_channel_awgn(torch_cuda, name, c):
     """AWGN frames generated on the GPU: info bits identical to the host Philox producer; the
@@ -851,9 +845,7 @@ def test_device_channel_awgn(torch_cuda, name, c):
     info, rx, out, _, err = _simulate(torch_cuda, Plan(c, SOFT), c, 5, first, nb, scaling)
     h_info, h_rx = ch.awgn_blocks(c, nb, scaling, 5, first_block=first)
     assert np.array_equal(info, h_info)
-    exact = np.mean(rx == h_rx)
-    assert exact >= 0.999, exact
-    assert np.allclose(rx, h_rx, rtol=1e-5, atol=1e-6)
+    _assert_samples_match(rx, h_rx)
     assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
     assert err == ch.count_bit_errors(c, info, out)
 
@@ -868,7 +860,7 @@ def test_device_channel_awgn_hard_demapper(torch_cuda, name, c):
     info, rx, out, _, err = _simulate(torch_cuda, Plan(c, SOFT), c, 9, 4321, nb, scaling, hard_demap=True)
     h_info, h_rx = ch.awgn_blocks(c, nb, scaling, 9, first_block=4321, hard_demap=True)
     assert np.array_equal(info, h_info)
-    assert np.mean(np.all(rx == h_rx, axis=2)) >= 0.999
+    _assert_samples_match(rx, h_rx, hard_demap=True)
     assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
     assert err == ch.count_bit_errors(c, info, out)
 
@@ -903,21 +895,15 @@ def test_device_channel_warm_up_changes_nothing(torch_cuda, decoder, c, channel)
 @pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["ref", "true"])
 def test_device_channel_k9_frames_path_equals_fused(torch_cuda, gen):
     """K = 9 soft at blen 40: ccv_simulate_device writes the frames (channel_frames) and decodes them
-    with the persistent kernel (x86 idiom: one lane per block; true parity: four lanes); the fused
-    multilane channel kernel (CCV_CHANNEL_FUSED=1) draws the same frames -- info, decoder input,
+    with the persistent kernel (x86 idiom: one lane per block; true parity: two lanes); the fused
+    multilane channel kernel (option channel_fused=1) draws the same frames -- info, decoder input,
     output and error count are identical, with and without the hard demapper, for ragged batches."""
-    import os
     c = K9.with_(gen_mode=gen)
     for nb, hard_demap in ((1, False), (200, False), (3 * 64 + 5, True)):
         runs = []
-        for fused in (False, True):
-            if fused:
-                os.environ["CCV_CHANNEL_FUSED"] = "1"
-            try:
-                runs.append(_simulate(torch_cuda, Plan(c, SOFT), c, 21, 7000 + nb, nb,
-                                      ch.noise_scaling(2.0), hard_demap=hard_demap))
-            finally:
-                os.environ.pop("CCV_CHANNEL_FUSED", None)
+        for fused in (0, 1):
+            runs.append(_simulate(torch_cuda, Plan(c, SOFT).set_option("channel_fused", fused), c, 21,
+                                  7000 + nb, nb, ch.noise_scaling(2.0), hard_demap=hard_demap))
         a, b = runs
         for k in (0, 1, 2):
             assert np.array_equal(a[k], b[k])
@@ -958,29 +944,22 @@ def test_device_channel_frames_only(torch_cuda, idx, channel):
         assert np.array_equal(info, h_info)
         if channel == HARD:
             assert np.array_equal(rx, h_rx)
-        elif demap:
-            assert np.mean(np.all(rx == h_rx, axis=2)) >= 0.999
         else:
-            assert np.mean(rx == h_rx) >= 0.999
-            assert np.allclose(rx, h_rx, rtol=1e-5, atol=1e-6)
+            _assert_samples_match(rx, h_rx, hard_demap=demap)
     plan.close()
 
 
 @pytest.mark.parametrize("channel", [SOFT, HARD])
 def test_device_channel_lds_vs_hbm_decisions(torch_cuda, channel):
-    """The LDS-decision channel kernel (CCV_CHANNEL_LDS_DECISIONS=1, the BSC default) and the
+    """The LDS-decision channel kernel (option channel_lds_decisions=1, the BSC default) and the
     HBM-scratch one (=0, the AWGN default) decode the same device-generated frames identically
     (outputs, path metrics, error counts)."""
-    import os
     param = 70000 if channel == HARD else ch.noise_scaling(1.0)
     for c in (K7, CODEBOOK[0], CODEBOOK[3].with_(blen=80), K7.with_(blen=1)):
         runs = []
-        for forced in ("1", "0"):
-            os.environ["CCV_CHANNEL_LDS_DECISIONS"] = forced
-            try:
-                runs.append(_simulate(torch_cuda, Plan(c, channel), c, 3, 5000, 777, param))
-            finally:
-                del os.environ["CCV_CHANNEL_LDS_DECISIONS"]
+        for forced in (1, 0):
+            plan = Plan(c, channel).set_option("channel_lds_decisions", forced)
+            runs.append(_simulate(torch_cuda, plan, c, 3, 5000, 777, param))
         a, b = runs
         for x, y in zip(a[:4], b[:4]):
             if channel == SOFT and x is a[3]:
@@ -989,10 +968,35 @@ def test_device_channel_lds_vs_hbm_decisions(torch_cuda, channel):
         assert a[4] == b[4]
 
 
+def test_plan_options_validate(torch_cuda):
+    """ccv_plan_set_option: unknown names, out-of-range values and options of another decoder fail
+    with a message; valid ones return the plan."""
+    from ccviterbi import K15, FanoPlan, StackPlan
+    plan = Plan(K7, SOFT)
+    assert plan.set_option("channel_lds_decisions", -1) is plan
+    for name, value, match in (("no_such_option", 1, "unknown option"), ("channel_fused", 2, "0 / 1"),
+                               ("stack_keys", 0, "stack-decoder plan"), ("fano_rows", 3, "Fano-decoder plan")):
+        with pytest.raises(Exception, match=match):
+            plan.set_option(name, value)
+    with pytest.raises(Exception, match="8 or 16"):
+        StackPlan(K15, HARD).set_option("stack_row_lanes", 4)
+    with pytest.raises(Exception, match="0..3"):
+        FanoPlan(K15, SOFT).set_option("fano_rows", 4)
+
+
 def test_device_channel_rejects_huge_noise(torch_cuda):
     plan = Plan(K7, SOFT)
     with pytest.raises(Exception, match="2\\^28"):
         plan.simulate_device(1, 0, 10, 3.0e8)
+
+
+def test_device_channel_frames_only_rejects_step_major(torch_cuda):
+    """Frames-only output is block-major: a step-major plan would decode it as scrambled input
+    (ADVICE r04), so ccv_simulate_device refuses it."""
+    plan = Plan(K7, SOFT, FLAG_STEP_MAJOR)
+    d_ch = torch_cuda.empty((4, K7.steps, 4), dtype=torch_cuda.float32, device="cuda")
+    with pytest.raises(Exception, match="step-major"):
+        plan.simulate_frames(1, 0, 4, ch.noise_scaling(3.0), d_ch)
 
 
 def test_device_channel_rejects_generic_codes(torch_cuda):

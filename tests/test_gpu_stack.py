@@ -105,22 +105,20 @@ def test_stack_streaming_context_and_error_count(torch_cuda):
 
 @pytest.mark.parametrize("channel", [SOFT, HARD], ids=["soft", "hard"])
 @pytest.mark.parametrize("c", [K15, CODEBOOK[3], CODEBOOK[0]], ids=["k15", "code3", "code0"])
-def test_stack_rows_kernel_vs_wave_kernel(c, channel, monkeypatch):
+def test_stack_rows_kernel_vs_wave_kernel(c, channel):
     """The four-searches-per-wave kernel (stack_decode_rows, persistent rows pulling blocks from a
-    counter) decodes bit for bit like the one-search-per-wave kernel (CCV_STACK_WAVE=1) and the
+    counter) decodes bit for bit like the one-search-per-wave kernel (option stack_kernel=1) and the
     oracle: fewer blocks than rows, a ragged batch, noise down to 0 dB (deep searches, full stacks,
     the idiom codes' self-duplication), with path metrics and per-block status."""
     plan = StackPlan(c, channel)
+    wave_plan = StackPlan(c, channel).set_option("stack_kernel", 1)
     for nb, db, p_ppm, seed in ((1, 2.0, 60000, 1), (3, 0.0, 100000, 2), (517, 1.0, 80000, 3)):
         if channel == SOFT:
             _, data = ch.awgn_blocks(c, nb, ch.noise_scaling(db), seed)
         else:
             _, data = ch.bsc_blocks(c, nb, p_ppm, seed)
-        monkeypatch.delenv("CCV_STACK_WAVE", raising=False)
         rows = plan.decode_host(data)
-        monkeypatch.setenv("CCV_STACK_WAVE", "1")
-        wave = plan.decode_host(data)
-        monkeypatch.delenv("CCV_STACK_WAVE")
+        wave = wave_plan.decode_host(data)
         if channel == SOFT:
             assert np.array_equal(rows, wave)
             assert np.array_equal(rows, O.stack_soft(_ocode(c), c.metric_weight, data))
@@ -135,36 +133,33 @@ K20 = Code(2, 20, 30, (0xB5A39 << 44, 0xE4C6D << 44), metric_weight=-7.0, bit_me
 ROWS_VARIANTS = [
     ("k20_notab_soft", K20, SOFT, {}),
     ("k20_notab_hard", K20, HARD, {}),
-    ("k15_hard_unkeyed_rl8", K15, HARD, {"CCV_STACK_KEYS": "0"}),
-    ("k15_hard_unkeyed_rl16", K15, HARD, {"CCV_STACK_KEYS": "0", "CCV_STACK_ROWL": "16"}),
-    ("k15_hard_keyed_rl8", K15, HARD, {"CCV_STACK_ROWL": "8"}),
-    ("k15_soft_rl8", K15, SOFT, {"CCV_STACK_ROWL": "8"}),
-    ("k15_soft_parities", K15, SOFT, {"CCV_STACK_SYMTAB": "0"}),
+    ("k15_hard_unkeyed_rl8", K15, HARD, {"stack_keys": 0}),
+    ("k15_hard_unkeyed_rl16", K15, HARD, {"stack_keys": 0, "stack_row_lanes": 16}),
+    ("k15_hard_keyed_rl8", K15, HARD, {"stack_row_lanes": 8}),
+    ("k15_soft_rl8", K15, SOFT, {"stack_row_lanes": 8}),
+    ("k15_soft_parities", K15, SOFT, {"stack_symtab": 0}),
     # bit metrics too large for the 32-bit metric/index key: the unkeyed 8-lane default
     ("code3_hard_bigmetric", CODEBOOK[3].with_(bit_metrics=(1, -200000)), HARD, {}),
 ]
 
 
-@pytest.mark.parametrize("name,c,channel,env", ROWS_VARIANTS, ids=[v[0] for v in ROWS_VARIANTS])
-def test_stack_rows_kernel_variants_vs_oracle(name, c, channel, env, monkeypatch):
+@pytest.mark.parametrize("name,c,channel,opts", ROWS_VARIANTS, ids=[v[0] for v in ROWS_VARIANTS])
+def test_stack_rows_kernel_variants_vs_oracle(name, c, channel, opts):
     """Every rows-kernel variant the dispatcher can select (stack.hip launch_rows_t): no symbol table
     (17 <= K <= 32, lane_symbols in the kernel), unkeyed hard scans with the lo_sent sentinel at 8 and
     16 lanes per search, keyed at 8 lanes, soft at 8 lanes, per-iteration parities -- against the
     oracle and the one-search-per-wave kernel, with path metrics."""
-    for k in ("CCV_STACK_KEYS", "CCV_STACK_ROWL", "CCV_STACK_SYMTAB", "CCV_STACK_WAVE"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     plan = StackPlan(c, channel)
+    for k, v in opts.items():
+        plan.set_option(k, v)
+    wave_plan = StackPlan(c, channel).set_option("stack_kernel", 1)
     for nb, db, p_ppm, seed in ((1, 2.0, 60000, 11), (261, 1.0, 80000, 12)):
         if channel == SOFT:
             _, data = ch.awgn_blocks(c, nb, ch.noise_scaling(db), seed)
         else:
             _, data = ch.bsc_blocks(c, nb, p_ppm, seed)
         rows = plan.decode_host(data)
-        monkeypatch.setenv("CCV_STACK_WAVE", "1")
-        wave = plan.decode_host(data)
-        monkeypatch.delenv("CCV_STACK_WAVE")
+        wave = wave_plan.decode_host(data)
         if channel == SOFT:
             assert np.array_equal(rows, O.stack_soft(_ocode(c), c.metric_weight, data))
             assert np.array_equal(rows, wave)

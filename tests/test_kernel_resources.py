@@ -47,11 +47,14 @@ def _kernel_metadata(tmp_path):
                     reason="needs the built library and the ROCm LLVM tools")
 def test_persistent_kernels_do_not_spill(tmp_path):
     meta = _kernel_metadata(tmp_path)
-    persistent = {k: v for k, v in meta.items() if "_persist" in k}
+    persistent = {k: v for k, v in meta.items() if "_persist" in k or "multi2_slot" in k}
     families = {f: [k for k in persistent if f in k] for f in
-                ("viterbi_soft_persist", "viterbi_hard_persist", "viterbi_multi_persist", "viterbi_wide_persist")}
+                ("viterbi_soft_persist", "viterbi_hard_persist", "viterbi_multi2_slot", "viterbi_wide_persist")}
     assert all(families.values()), {f: len(v) for f, v in families.items()}
-    bad = {k: v for k, v in persistent.items() if v[1] or v[2]}
+    # the two-lane true-parity K = 9 kernel holds 256 VGPRs and spills one register outside its main
+    # loop; every other persistent kernel spills nothing
+    bad = {k: v for k, v in persistent.items()
+           if ((v[1] > 1 or v[2] > 8) if "multi2_slot" in k else (v[1] or v[2]))}
     assert not bad, bad
     # the K = 9 one-lane kernel: two waves per SIMD (the launch bounds' waves_per_eu(2))
     assert all(v[0] <= 256 for k, v in persistent.items() if "wide_persist" in k)
@@ -78,8 +81,8 @@ def _code_objects(tmp_path):
                     reason="needs the built library and the ROCm LLVM tools")
 def test_true_parity_k9_slot_kernels_have_no_cross_lane_valu(tmp_path):
     """On gfx950 one DPP / permlane VALU instruction halves a wave's VALU rate for hundreds of
-    instructions; the production true-parity K = 9 kernels (two lanes per block, and
-    the four-lane A/B form, both with XSWZ) move data between lanes only through ds_swizzle. A DPP or
+    instructions; the production true-parity K = 9 kernel (two lanes per block) moves
+    data between lanes only through ds_swizzle. A DPP or
     permlane instruction creeping back in (a compiler choice or an edit) keeps every result bit-exact
     and costs ~8 %: caught here."""
     found = {}
@@ -88,9 +91,9 @@ def test_true_parity_k9_slot_kernels_have_no_cross_lane_valu(tmp_path):
                              text=True).stdout
         for m in re.finditer(r"^[0-9a-f]+ <(\S+)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", dis, re.S | re.M):
             name, body = m.group(1), m.group(2)
-            # viterbi_multi2_slot<C, 40, true, 7> and viterbi_multi_slot<C, 40, 3, true, 0, 3>
-            if ("viterbi_multi2_slot" in name and "Lb1E" in name) or ("viterbi_multi_slot" in name and "Li3ELb1E" in name):
+            # viterbi_multi2_slot<C, 40, 7>
+            if "viterbi_multi2_slot" in name:
                 found[name] = len(re.findall(r"_dpp|\bdpp|permlane", body)), body.count("ds_swizzle")
-    assert len(found) == 2, list(found)
+    assert len(found) == 1, list(found)
     for name, (xlane, swz) in found.items():
         assert xlane == 0 and swz > 0, (name, xlane, swz)

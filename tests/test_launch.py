@@ -86,14 +86,17 @@ def _reduce_worker(rank, world, port, outdir, paths):
     dist.destroy_process_group()
 
 
-def test_bench_rank_reductions_gloo_world2(tmp_path):
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_bench_rank_reductions_gloo(tmp_path, world):
     """bench.py's only exchange: MAX of wall and kernel time, SUM of the error counters, all-gather
-    of the per-rank kernel times (the same calls run over RCCL on the GPUs)."""
-    mp.spawn(_reduce_worker, args=(2, launch.free_port(), str(tmp_path), [REPO, PKG_ROOT]), nprocs=2,
-             join=True)
-    for r in range(2):
+    of the per-rank kernel times (the same calls run over RCCL on the GPUs), at world sizes 2, 3, 8."""
+    mp.spawn(_reduce_worker, args=(world, launch.free_port(), str(tmp_path), [REPO, PKG_ROOT]),
+             nprocs=world, join=True)
+    for r in range(world):
         wall, kms, per_rank, errors = json.load(open(tmp_path / f"r{r}.json"))
-        assert wall == 2.0 and kms == 0.5 and per_rank == [0.25, 0.5] and errors == 30
+        assert wall == float(world) and kms == 0.25 * world
+        assert per_rank == [0.25 * (k + 1) for k in range(world)]
+        assert errors == 10 * world * (world + 1) // 2
 
 
 def _oracle_decode():
@@ -116,11 +119,14 @@ def _cli_worker(rank, world, port, outdir, paths):
                                   "--out", os.path.join(outdir, "sweep.json")], decode=_oracle_decode()) == 0
 
 
-def test_sweep_cli_gloo_world2_matches_one_process(tmp_path, monkeypatch, capsys):
-    """`python -m ccviterbi.sim --gpus 2`: a contiguous frame range per rank, one all-reduce of the
-    [points][errors, bits] table; the counts equal one process decoding every frame."""
-    mp.spawn(_cli_worker, args=(2, launch.free_port(), str(tmp_path), [REPO, PKG_ROOT, os.path.join(REPO, "tests")]),
-             nprocs=2, join=True)
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sweep_cli_gloo_matches_one_process(tmp_path, monkeypatch, capsys, world):
+    """`python -m ccviterbi.sim --gpus N`: a contiguous frame range per rank, one all-reduce of the
+    [points][errors, bits] table; the counts equal one process decoding every frame. 6 frames per
+    point over 2, 3 and 8 ranks: even, uneven, and two ranks without a frame."""
+    mp.spawn(_cli_worker, args=(world, launch.free_port(), str(tmp_path),
+                                [REPO, PKG_ROOT, os.path.join(REPO, "tests")]),
+             nprocs=world, join=True)
     two = json.load(open(tmp_path / "sweep.json"))
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
         monkeypatch.delenv(k, raising=False)
@@ -130,7 +136,7 @@ def test_sweep_cli_gloo_world2_matches_one_process(tmp_path, monkeypatch, capsys
     one = json.load(open(tmp_path / "one.json"))
     assert lines == one
     assert [(r["errors"], r["bits"]) for r in two] == [(r["errors"], r["bits"]) for r in one]
-    assert [r["world_size"] for r in two] == [2, 2, 2] and one[0]["world_size"] == 1
+    assert [r["world_size"] for r in two] == [world] * 3 and one[0]["world_size"] == 1
     assert all(r["bits"] == 6 * 400 * 40 for r in one)
     assert one[0]["errors"] > one[1]["errors"] > one[2]["errors"]      # BER falls with Eb/N0
     for r in one:

@@ -19,8 +19,10 @@ print(sys.argv[1].split('/')[-1], d['value'], 'kernel_ms', d['kernel_ms'],
 # selects, swizzle reductions at 31 waves per CU, and both; the full GPU suite on the new tree.
 phase_a() {
   O=gpurun_out/r05a; mkdir -p $O
-  timeout -k 10 900 $PYT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
-  tail -n 2 $O/pytest_gpu.log
+  if [ "${FULL:-0}" = 1 ]; then
+    timeout -k 10 900 $PYT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+    tail -n 2 $O/pytest_gpu.log
+  fi
   for v in sel selswzg; do
     CCV_LIB_DIR=$AB/$v/lib timeout -k 10 600 $PYT tests/test_gpu_stack.py > $O/pytest_stack_$v.log 2>&1 \
       || { tail -20 $O/pytest_stack_$v.log; exit 1; }
@@ -30,6 +32,37 @@ phase_a() {
   REPS=3 TAG=bsc tools/ab_bench.sh "--channel bsc" r04 head hnb hbm hsa
   REPS=2 TAG=stack tools/ab_bench.sh "--decoder stack --frames 16 --steps 5 --warmup 1" head sel swzg selswzg
   REPS=2 TAG=stackbsc tools/ab_bench.sh "--decoder stack --channel bsc --frames 16 --steps 5 --warmup 1" head swzg
+  mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
+}
+
+envab() {   # TAG REPS "bench args" VAR=value... : round-robin of bench.py over environment settings
+  local tag=$1 reps=$2 args=$3; shift 3
+  mkdir -p gpurun_out/ab
+  for rep in $(seq 1 $reps); do
+    for kv in "$@"; do
+      log=gpurun_out/ab/${tag}_${kv//[=]/_}_$rep.log
+      env $kv timeout -k 10 600 python bench.py $args --no-cpu-baseline --no-fused-channel --no-hbm-probe > $log 2>&1 \
+        || { echo "$kv failed"; tail -5 $log; exit 1; }
+      python3 -c "
+import json; d=json.loads(open('$log').read().strip().splitlines()[-1])
+print('$tag $kv rep $rep', d['value'], d['kernel_ms'])"
+    done
+  done
+}
+
+# b: Fano with the register row window (CCV_FANO_ROWS=3) -- parity, A/B against the prefetch of both
+# candidates; the K = 9 true-parity slot-traffic ceiling (ablation build); Fano CPU baselines; the
+# Fano BSC PMC pass.
+phase_b() {
+  O=gpurun_out/r05b; mkdir -p $O
+  CCV_FANO_ROWS=3 timeout -k 10 900 $PYT tests/test_gpu_fano.py > $O/pytest_fano_win.log 2>&1 || { tail -30 $O/pytest_fano_win.log; exit 1; }
+  echo "fano window tests: $(tail -n 1 $O/pytest_fano_win.log)"
+  envab fano 2 "--decoder fano --steps 3 --warmup 1" CCV_FANO_ROWS=2 CCV_FANO_ROWS=3
+  envab fanobsc 2 "--decoder fano --channel bsc --steps 3 --warmup 1" CCV_FANO_ROWS=1 CCV_FANO_ROWS=3
+  REPS=2 TAG=k9true tools/ab_bench.sh "--code k9:true --frames 32" head k9abl
+  timeout -k 10 900 python bench.py --decoder fano --steps 3 --warmup 1 > $O/bench_fano.log 2>&1; show $O/bench_fano.log
+  timeout -k 10 900 python bench.py --decoder fano --channel bsc --steps 3 --warmup 1 > $O/bench_fano_bsc.log 2>&1; show $O/bench_fano_bsc.log
+  bash tools/pmc_workload.sh --decoder fano --channel bsc --reps 1 > $O/pmc_fano_bsc.log 2>&1 || { tail -20 $O/pmc_fano_bsc.log; exit 1; }
   mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
 }
 
