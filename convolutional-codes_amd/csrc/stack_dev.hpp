@@ -554,13 +554,13 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
         else row_max_min<RL>(mx, mn);
         uint32_t cand = kStackDepth;
         c2 = kStackDepth;
-        if constexpr (CCV_STACK_SGPR_SEL && kRowSlots == 4) {
+        if constexpr (CCV_STACK_SGPR_SEL && kRowSlots == 4 && !HARD) {
           // the eight compares into SGPR pairs first, then the selects: hipcc's form is a serial
           // v_cmp -> VCC -> v_cndmask_e32 chain with an s_nop 1 in each link (2 wait states after a
           // VALU SGPR write on gfx950), and a VCC compare/select pair costs ~7 ns per instruction
           // (profiles/r02_rates_argmin.txt). Here every select reads a mask written >= 2 VALU
           // instructions earlier: no wait state, no VCC. Same result: the lowest k with
-          // met[k] == mx (resp. mn) wins.
+          // met[k] == mx (resp. mn) wins. Float metrics only (the compare is v_cmp_eq_f32).
           const uint32_t i0 = (uint32_t)(l * kRowSlots);
           uint64_t e0, e1, e2, e3, f0, f1, f2, f3;
           uint32_t tmp;
