@@ -364,6 +364,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0xC0DE)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline work budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="plan option (ccv_plan_set_option, include/ccv.h) for A/B runs; repeatable")
     ap.add_argument("--no-hbm-probe", action="store_true",
                     help="skip the achievable-HBM probe (A/B runs of builds that predate it)")
     ap.add_argument("--no-fused-channel", action="store_true",
@@ -421,6 +423,9 @@ def main(argv=None):
         plan = Plan(code, chan, (FLAG_STEP_MAJOR if args.layout == "step" else 0) |
                     (FLAG_GLOBAL_DECISIONS if args.decisions == "hbm" else 0) |
                     (FLAG_NO_PERSISTENT if args.persistent == "off" else 0))
+    for opt in args.option:
+        name, value = opt.split("=", 1)
+        plan.set_option(name, int(value))
     plan.reserve(nb)
     stream = torch.cuda.current_stream()
 
@@ -576,6 +581,7 @@ def main(argv=None):
                 "parallelism": f"dp{world} (frames sharded, counters all-reduced once)",
                 "kernel": plan.kernel,
                 "variant": getattr(plan, "variant", plan.kernel),
+                **({"options": dict(o.split("=", 1) for o in args.option)} if args.option else {}),
                 "decisions": plan.decisions,
                 "input_layout": ("block-major [nb][T] symbols (reference)" if hard else
                                  "block-major [nb][T][2^n] (reference)" if args.layout == "block"

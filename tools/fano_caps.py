@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Fano two-pass schedule sweep: search-length percentiles of the bench workload (K=15, 104 frames)
-and the decode time for several park caps (CCV_FANO_CAP; 0 = one pass), interleaved repeats.
+and the decode time for several park caps (plan option fano_cap; 0 = one pass), interleaved repeats.
 usage: fano_caps.py [--ebn0 4] [--channel awgn|bsc] [--frames 104] caps..."""
 import argparse
 import os
@@ -34,7 +34,7 @@ def main():
     d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
     d_it = torch.zeros(nb, dtype=torch.int32, device="cuda")
     plan = FanoPlan(c, HARD if hard else SOFT)
-    os.environ["CCV_FANO_CAP"] = "0"
+    plan.set_option("fano_cap", 0)
     plan.decode_fano_device(d_rx, nb, d_out, d_iterations=d_it)
     torch.cuda.synchronize()
     it = d_it.cpu().numpy()
@@ -45,7 +45,7 @@ def main():
     times = {cap: [] for cap in args.caps}
     for _ in range(args.reps):
         for cap in args.caps:
-            os.environ["CCV_FANO_CAP"] = cap
+            plan.set_option("fano_cap", int(cap))
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             plan.decode_fano_device(d_rx, nb, d_out)

@@ -23,7 +23,7 @@ phase_a() {
     timeout -k 10 900 $PYT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
     tail -n 2 $O/pytest_gpu.log
   fi
-  for v in sel selswzg; do
+  for v in sel swzg selswzg; do
     CCV_LIB_DIR=$AB/$v/lib timeout -k 10 600 $PYT tests/test_gpu_stack.py > $O/pytest_stack_$v.log 2>&1 \
       || { tail -20 $O/pytest_stack_$v.log; exit 1; }
     echo "stack tests $v: $(tail -n 1 $O/pytest_stack_$v.log)"
@@ -35,34 +35,45 @@ phase_a() {
   mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
 }
 
-envab() {   # TAG REPS "bench args" VAR=value... : round-robin of bench.py over environment settings
+optab() {   # TAG REPS "bench args" "opts"... : round-robin of bench.py over plan-option sets ("-" = defaults)
   local tag=$1 reps=$2 args=$3; shift 3
   mkdir -p gpurun_out/ab
   for rep in $(seq 1 $reps); do
-    for kv in "$@"; do
-      log=gpurun_out/ab/${tag}_${kv//[=]/_}_$rep.log
-      env $kv timeout -k 10 600 python bench.py $args --no-cpu-baseline --no-fused-channel --no-hbm-probe > $log 2>&1 \
-        || { echo "$kv failed"; tail -5 $log; exit 1; }
+    for o in "$@"; do
+      local flags="" name="default"
+      if [ "$o" != "-" ]; then name=${o// /_}; for kv in $o; do flags="$flags --option $kv"; done; fi
+      log=gpurun_out/ab/${tag}_${name//=/}_$rep.log
+      timeout -k 10 600 python bench.py $args $flags --no-cpu-baseline --no-fused-channel --no-hbm-probe > $log 2>&1 \
+        || { echo "$o failed"; tail -5 $log; exit 1; }
       python3 -c "
 import json; d=json.loads(open('$log').read().strip().splitlines()[-1])
-print('$tag $kv rep $rep', d['value'], d['kernel_ms'])"
+print('$tag [$o] rep $rep', d['value'], d['kernel_ms'])"
     done
   done
 }
 
-# b: Fano with the register row window (CCV_FANO_ROWS=3) -- parity, A/B against the prefetch of both
-# candidates; the K = 9 true-parity slot-traffic ceiling (ablation build); Fano CPU baselines; the
-# Fano BSC PMC pass.
+# b: Fano with the register row window (fano_rows=3: parity in test_gpu_fano.py, A/B against the
+# prefetch of both candidates); the K = 9 true-parity slot-traffic ceiling (ablation build); stack
+# decoder options and PMC of the stack variants; Fano CPU baselines and the Fano BSC PMC pass; the
+# HBM probe variants.
 phase_b() {
   O=gpurun_out/r05b; mkdir -p $O
-  CCV_FANO_ROWS=3 timeout -k 10 900 $PYT tests/test_gpu_fano.py > $O/pytest_fano_win.log 2>&1 || { tail -30 $O/pytest_fano_win.log; exit 1; }
-  echo "fano window tests: $(tail -n 1 $O/pytest_fano_win.log)"
-  envab fano 2 "--decoder fano --steps 3 --warmup 1" CCV_FANO_ROWS=2 CCV_FANO_ROWS=3
-  envab fanobsc 2 "--decoder fano --channel bsc --steps 3 --warmup 1" CCV_FANO_ROWS=1 CCV_FANO_ROWS=3
+  timeout -k 10 120 tools/hbm_probe > $O/hbm_probe.txt 2>&1 || { cat $O/hbm_probe.txt; exit 1; }
+  cat $O/hbm_probe.txt
+  timeout -k 10 900 $PYT tests/test_gpu_fano.py > $O/pytest_fano.log 2>&1 || { tail -30 $O/pytest_fano.log; exit 1; }
+  echo "fano tests: $(tail -n 1 $O/pytest_fano.log)"
+  optab fano 2 "--decoder fano --steps 3 --warmup 1" "fano_rows=2" "fano_rows=3"
+  optab fanobsc 2 "--decoder fano --channel bsc --steps 3 --warmup 1" "fano_rows=1" "fano_rows=3"
   REPS=2 TAG=k9true tools/ab_bench.sh "--code k9:true --frames 32" head k9abl
+  optab stack 2 "--decoder stack --frames 16 --steps 5 --warmup 1" "-" "stack_symtab=0" "stack_row_lanes=8"
+  for v in head swzg; do
+    dir=$PWD/convolutional-codes_amd/build_ab/$v/lib; [ $v = head ] && dir=$PWD/convolutional-codes_amd/lib
+    CCV_LIB_DIR=$dir PMC_TAG=$v PMC_JSON=gpurun_out/pmc/pmc_stack_$v.json bash tools/pmc_workload.sh --decoder stack --frames 16 --reps 2 \
+        > $O/pmc_stack_$v.log 2>&1 || { tail -20 $O/pmc_stack_$v.log; exit 1; }
+  done
+  bash tools/pmc_workload.sh --decoder fano --channel bsc --reps 1 > $O/pmc_fano_bsc.log 2>&1 || { tail -20 $O/pmc_fano_bsc.log; exit 1; }
   timeout -k 10 900 python bench.py --decoder fano --steps 3 --warmup 1 > $O/bench_fano.log 2>&1; show $O/bench_fano.log
   timeout -k 10 900 python bench.py --decoder fano --channel bsc --steps 3 --warmup 1 > $O/bench_fano_bsc.log 2>&1; show $O/bench_fano_bsc.log
-  bash tools/pmc_workload.sh --decoder fano --channel bsc --reps 1 > $O/pmc_fano_bsc.log 2>&1 || { tail -20 $O/pmc_fano_bsc.log; exit 1; }
   mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
 }
 

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--p-ppm", type=int, default=50000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0xC0DE)
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE")
     args = ap.parse_args()
     import torch
 
@@ -52,6 +53,9 @@ def main():
         plan = FanoPlan(code, chan)
     else:
         plan = Plan(code, chan, FLAG_STEP_MAJOR if args.layout == "step" else 0)
+    for opt in args.option:
+        name, value = opt.split("=", 1)
+        plan.set_option(name, int(value))
     plan.reserve(nb)
     for _ in range(args.reps):
         plan.decode_device(d_rx, nb, d_out, d_info=d_info, d_errors=d_err, stream=torch.cuda.current_stream())
