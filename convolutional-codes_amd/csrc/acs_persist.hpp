@@ -439,8 +439,13 @@ __device__ __forceinline__ uint32_t lds_read_u8(uint32_t addr) {
 #ifndef CCV_HARD_SYM_AHEAD
 #define CCV_HARD_SYM_AHEAD 0
 #endif
+// metric type of the BSC persistent kernel: 2 = uint16_t (v_add_u16 / v_min_u16), 3 = fp32 (exact for
+// these small integer metrics: the soft kernel's v_add_f32 / v_min_f32 / v_sub_f32 stream)
+#ifndef CCV_HARD_MMODE
+#define CCV_HARD_MMODE 2
+#endif
 
-template <CodeSpec C, int BLEN, int MMODE = 2>
+template <CodeSpec C, int BLEN, int MMODE = CCV_HARD_MMODE>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void viterbi_hard_persist(RegArgs a, int ngroups) {
   constexpr int S = 1 << (C.K - 1);
@@ -499,8 +504,13 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
     // scheduler); 0 = H16 inline-asm ops (round 2 first cut: hipcc puts an s_nop 0 after every
     // inline-asm VALU whose result is read next, 1,612 per group, 6 % slower); 1 = u32 (v_bcnt-folded
     // adds and v_min_u32, half rate: 25 % slower). tools/persist_bench abh.
-    using MT = typename std::conditional<MMODE == 1, uint32_t,
-                                         typename std::conditional<MMODE >= 2, uint16_t, H16>::type>::type;
+    //  3 = fp32: every metric here is a small integer (<= n * T < 2^24 after the growth steps, the
+    //  unreachable growth states the constant 0xFF00), so fp32 adds, mins and the sign of m1 - m0 are
+    //  exact and give the u16 decisions bit for bit.
+    using MT = typename std::conditional<
+        MMODE == 3, float,
+        typename std::conditional<MMODE == 1, uint32_t,
+                                  typename std::conditional<MMODE >= 2, uint16_t, H16>::type>::type>::type;
     MT M[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) M[s] = MT{(MT)(s ? 0xFF00u : 0u)};   // viterbi-decoder.c:225-228
@@ -534,7 +544,15 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
         constexpr int t = c * PF + u;
         if constexpr (t < T) {
           MT BM[NS];
-          if constexpr (CCV_HARD_BM_PAIRS != 0 && NS == 4) {
+          if constexpr (MMODE == 3 && NS == 4) {
+            // popcount(k ^ s) over n = 2 bits as floats: k and k ^ 3 sum to 2
+            const float p0 = (float)__builtin_popcount(sym[u] & kMask);
+            const float p1 = (float)__builtin_popcount((sym[u] ^ 1u) & kMask);
+            BM[0] = p0;
+            BM[1] = p1;
+            BM[2] = 2.0f - p1;
+            BM[3] = 2.0f - p0;
+          } else if constexpr (CCV_HARD_BM_PAIRS != 0 && NS == 4) {
             // popcount(k ^ s) over n = 2 bits: k and k ^ 3 sum to 2
             const uint32_t p0 = (uint32_t)__builtin_popcount(sym[u] & kMask);
             const uint32_t p1 = (uint32_t)__builtin_popcount((sym[u] ^ 1u) & kMask);
@@ -566,14 +584,20 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
       (chunk_at.template operator()<cs>(), ...);
     }(std::make_integer_sequence<int, NCH>{});
 
-    uint32_t Mu[S];
+    uint32_t best, st;
+    if constexpr (MMODE == 3) {
+      float bf;
+      st = (uint32_t)argmin_state<S, float>(M, 65280.0f, bf);
+      best = (uint32_t)bf;
+    } else {
+      uint32_t Mu[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      if constexpr (MMODE >= 1) Mu[s] = M[s];
-      else Mu[s] = M[s].v & 0xFFFFu;
+      for (int s = 0; s < S; ++s) {
+        if constexpr (MMODE >= 1) Mu[s] = M[s];
+        else Mu[s] = M[s].v & 0xFFFFu;
+      }
+      st = (uint32_t)argmin_state<S, uint32_t>(Mu, 0xFF00u, best);
     }
-    uint32_t best;
-    const uint32_t st = (uint32_t)argmin_state<S, uint32_t>(Mu, 0xFF00u, best);
     if (a.path_metric) a.path_metric[b] = (int32_t)best;
     const uint64_t bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
     errors += emit_block<T, BLEN>(a, b, bits, info);

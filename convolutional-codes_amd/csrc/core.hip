@@ -316,30 +316,32 @@ hipError_t launch_service(const ccv::GenericArgs& a, const ccv_plan& p, ccv::Ser
 }
 
 // The achievable-HBM ceiling of the roofline ("a measured copy-kernel ceiling"): a
-// streaming pass over a buffer in 16-byte lanes, four global_load_dwordx4 in flight per lane, each
-// wave-instruction 1 KiB of consecutive bytes. COPY stores every vector (global_store_dwordx4: the
-// float4 copy of MI355X_MICROARCH.md, 6.29 TB/s read + write there); otherwise the loads are folded
-// into one XOR per lane so nothing is stored but a never-taken sink write (read-only stream, the
-// access the decode kernels make of their input).
-template <bool COPY>
-__global__ __launch_bounds__(256) void hbm_stream(const uint4* __restrict__ src, uint4* __restrict__ dst,
+// streaming pass over a buffer in 16-byte lanes, U non-temporal global_load_dwordx4 in flight per
+// lane, each wave-instruction 1 KiB of consecutive bytes. COPY stores every vector (non-temporal
+// global_store_dwordx4); otherwise the loads are folded into one XOR per lane and nothing is stored
+// but a never-taken sink write (the read-only stream the decode kernels make of their input). The
+// variants measured on the 1.9 GB headline batch (tools/hbm_probe.hip, profiles/r05b/hbm_probe.txt):
+// read, non-temporal, U = 8: 7.05-7.11 TB/s (plain loads 6.16-6.45); copy, non-temporal, U = 4:
+// 5.66-5.75 TB/s (plain 5.03-5.39) -- both above the guide's 6.29 TB/s float4 copy figure.
+typedef uint32_t probe_u32x4 __attribute__((ext_vector_type(4)));
+template <bool COPY, int U>
+__global__ __launch_bounds__(256) void hbm_stream(const probe_u32x4* __restrict__ src, probe_u32x4* __restrict__ dst,
                                                   size_t n16, uint32_t* sink) {
-  constexpr int U = 4;
   const size_t stride = (size_t)gridDim.x * 256 * U;
   uint32_t acc = 0;
   size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x;
   for (; i + (U - 1) * 256 < n16; i += stride) {
-    uint4 v[U];
+    probe_u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = src[i + u * 256];
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + i + u * 256);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if constexpr (COPY) dst[i + u * 256] = v[u];
+      if constexpr (COPY) __builtin_nontemporal_store(v[u], dst + i + u * 256);
       else acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
   }
   for (; i < n16; i += 256) {   // the ragged end of the buffer
-    const uint4 v = src[i];
+    const probe_u32x4 v = src[i];
     if constexpr (COPY) dst[i] = v;
     else acc ^= v.x ^ v.y ^ v.z ^ v.w;
   }
@@ -359,15 +361,15 @@ int ccv_hbm_probe(int mode, void* dst, const void* src, size_t bytes, uint32_t* 
   int dev = 0, cus = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  // 8 workgroups of 4 waves per CU: 32 waves per CU, 16 KiB of loads in flight per wave
+  // 8 workgroups of 4 waves per CU (4 to 16 measure the same)
   const size_t want = (n16 + 1023) / 1024;
   const unsigned grid = (unsigned)(want < (size_t)cus * 8 ? want : (size_t)cus * 8);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mode == 0)
-    hipLaunchKernelGGL((hbm_stream<true>), dim3(grid), dim3(256), 0, s, static_cast<const uint4*>(src),
-                       static_cast<uint4*>(dst), n16, sink);
+    hipLaunchKernelGGL((hbm_stream<true, 4>), dim3(grid), dim3(256), 0, s, static_cast<const probe_u32x4*>(src),
+                       static_cast<probe_u32x4*>(dst), n16, sink);
   else
-    hipLaunchKernelGGL((hbm_stream<false>), dim3(grid), dim3(256), 0, s, static_cast<const uint4*>(src),
+    hipLaunchKernelGGL((hbm_stream<false, 8>), dim3(grid), dim3(256), 0, s, static_cast<const probe_u32x4*>(src),
                        nullptr, n16, sink);
   HIP_TRY(hipGetLastError());
   return 0;
@@ -491,7 +493,7 @@ int ccv_plan_set_option(ccv_plan* p, const char* name, long long value) {
   }
   if (n == "fano_rows" || n == "fano_symtab" || n == "fano_order" || n == "fano_cap" || n == "fano_count_moves") {
     if (need(p->fano, "a Fano-decoder plan option")) return -1;
-    if (n == "fano_rows") { if (need(in(-1, 3), "-1 (auto) or 0..3")) return -1; p->opt.fano_rows = (int)value; }
+    if (n == "fano_rows") { if (need(in(-1, 2), "-1 (auto) or 0..2")) return -1; p->opt.fano_rows = (int)value; }
     if (n == "fano_symtab") { if (need(in(-1, 1), "-1 (auto), 0 / 1")) return -1; p->opt.fano_symtab = (int)value; }
     if (n == "fano_order") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.fano_order = (int)value; }
     if (n == "fano_cap") { if (need(in(-1, 0xFFFFFFFFll), "-1 (default) or moves")) return -1; p->opt.fano_cap = value; }

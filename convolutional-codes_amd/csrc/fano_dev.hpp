@@ -101,6 +101,14 @@ __global__ void fano_score(const float* in, int T, int nblocks, float* key, uint
 }
 
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
+
+// CCV_FANO_FLAGREG (A/B, round 5): a node's flags (selected branch, decoded input) as bits of two
+// 64-bit masks per lane instead of a byte per node in LDS -- the node arrays shrink from 5 to 4 bytes
+// per node, 9 -> 11 waves per CU at K = 15 (T + 1 <= 64 required).
+#ifndef CCV_FANO_FLAGREG
+#define CCV_FANO_FLAGREG 0
+#endif
+__host__ __device__ constexpr size_t fano_flag_bytes_per_node() { return CCV_FANO_FLAGREG ? 0 : 1; }
 constexpr int kFanoThreads = 64;
 
 // Received-symbol access per lane (RM):
@@ -110,11 +118,9 @@ constexpr int kFanoThreads = 64;
 //     cur + 1) and the lane keeps its own node's row in registers, so the load latency overlaps the
 //     pass instead of following it (hard input or rate 1/2: a row is a byte or a float4).
 //   kRowsLds: as kRowsGlobal, the block's rows copied into LDS when the lane takes the block.
-//   kRowsWindow: the rows of cur - 1, cur and cur + 1 stay in registers; a move shifts the window
-//     and issues ONE load, the row beyond its new edge, which the lane first reads at the end of its
-//     NEXT pass -- a whole pass of latency hiding instead of part of one, and one load per pass
-//     instead of two (round 5; rate 1/2 soft input).
-constexpr int kRowsDirect = 0, kRowsGlobal = 2, kRowsLds = 1, kRowsWindow = 3;
+// (Round 5 measured and removed a register window of rows cur - 1, cur, cur + 1 with one load per
+// move issued a pass ahead: 67 -> 48 Mbit/s soft, 222 -> 156 BSC, profiles/r05b/.)
+constexpr int kRowsDirect = 0, kRowsGlobal = 2, kRowsLds = 1;
 template <bool HARD, int NP>
 struct FanoRow;
 template <int NP>
@@ -151,7 +157,6 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   using ST = typename std::conditional<W32, uint32_t, uint64_t>::type;
   static_assert(RM == kRowsDirect || HARD || NP == 2, "rows of received symbols are a byte or a float4");
   constexpr bool ROWS = RM != kRowsDirect;
-  constexpr bool WIN = RM == kRowsWindow;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const int T = a.T, K = a.K, n = a.n;
@@ -160,7 +165,30 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   MT* metric = reinterpret_cast<MT*>(smem);
   uint8_t* flags = smem + (size_t)(T + 1) * kFanoThreads * sizeof(MT);   // sel | dec << 1
   // rows: [T][64] float4 (soft) or bytes (hard), after the flags (16-byte aligned)
-  unsigned char* rows = smem + (((size_t)(T + 1) * kFanoThreads * (sizeof(MT) + 1) + 15) & ~(size_t)15);
+  unsigned char* rows =
+      smem + (((size_t)(T + 1) * kFanoThreads * (sizeof(MT) + fano_flag_bytes_per_node()) + 15) & ~(size_t)15);
+#if CCV_FANO_FLAGREG
+  uint64_t fsel = 0, fdec = 0;   // bit d: node d's selected branch / decoded input
+  (void)flags;
+#endif
+  // a node's flags byte (sel | dec << 1): LDS, or the lane's two masks
+  auto flag_get = [&](int d) -> uint32_t {
+#if CCV_FANO_FLAGREG
+    return (uint32_t)((fsel >> d) & 1u) | ((uint32_t)((fdec >> d) & 1u) << 1);
+#else
+    return flags[d * kFanoThreads + lane];
+#endif
+  };
+  // store v at node d when `write` (otherwise nothing; the LDS form writes the spare row T instead)
+  auto flag_put = [&](bool write, int d, uint32_t v) {
+#if CCV_FANO_FLAGREG
+    const uint64_t m = write ? (1ull << d) : 0ull;
+    fsel = (fsel & ~m) | ((v & 1u) ? m : 0ull);
+    fdec = (fdec & ~m) | ((v & 2u) ? m : 0ull);
+#else
+    flags[(write ? d : T) * kFanoThreads + lane] = (uint8_t)v;
+#endif
+  };
   uint64_t poly[kMaxN];
 #pragma unroll
   for (int k = 0; k < kMaxN; ++k) poly[k] = a.poly[k];
@@ -242,10 +270,6 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   bool inback = false, moved = false;
   uint32_t moves = 0, spass = 0;
   FanoRow<HARD, NP> row0{};   // received row of node cur
-  // WIN: rows of cur - 1 (rwa) and cur + 1 (rwb), except that the side of the last move is still in
-  // flight in rwn (pdir = +1: rwn is cur + 1's row, -1: cur - 1's, 0: no load pending)
-  FanoRow<HARD, NP> rwa{}, rwb{}, rwn{};
-  int pdir = 0;
   auto as_bits = [](MT v) -> uint32_t {
     if constexpr (HARD) return (uint32_t)v;
     else return __float_as_uint(v);
@@ -264,7 +288,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     uint8_t* pf = a.park_flags + (size_t)k * (T + 1);
     for (int d = 0; d <= frontier; ++d) {
       pm[d] = metric[d * kFanoThreads + lane];
-      pf[d] = flags[d * kFanoThreads + lane];
+      pf[d] = (uint8_t)flag_get(d);
     }
     h[0] = b;
     h[1] = (uint32_t)cur;
@@ -300,9 +324,12 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     frontier = (int)h[2];
     const MT* pm = static_cast<const MT*>(a.park_metric) + (size_t)slot * (T + 1);
     const uint8_t* pf = a.park_flags + (size_t)slot * (T + 1);
+#if CCV_FANO_FLAGREG
+    fsel = fdec = 0;
+#endif
     for (int d = 0; d <= frontier; ++d) {
       metric[d * kFanoThreads + lane] = pm[d];
-      flags[d * kFanoThreads + lane] = pf[d];
+      flag_put(true, d, pf[d]);
     }
     st = (ST)((uint64_t)h[3] | ((uint64_t)h[4] << 32));
     mcur = from_bits(h[5]);
@@ -317,11 +344,6 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     moves = h[11];
     spass = 0;
     if constexpr (ROWS) row0 = row_at(cur);
-    if constexpr (WIN) {
-      rwa = row_at(cur > 0 ? cur - 1 : 0);
-      rwb = row_at(cur + 1 < T ? cur + 1 : T - 1);
-      pdir = 0;
-    }
   };
   // start a search (:108-124 reset, then the root's branch metrics)
   auto start = [&]() {
@@ -334,11 +356,6 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     load_rows();
     spass = 0;
     if constexpr (ROWS) row0 = row_at(0);
-    if constexpr (WIN) {
-      rwa = row0;
-      rwb = row_at(1 < T ? 1 : 0);
-      pdir = 0;
-    }
     metric[lane] = (MT)0;
     cur = 0;
     frontier = 0;
@@ -349,7 +366,10 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     node_metrics(rx, 0, 0, row0, tm0, tm1, sw);
     sel = 0;
     dec = sw;
-    flags[lane] = (uint8_t)(dec << 1);
+#if CCV_FANO_FLAGREG
+    fsel = fdec = 0;
+#endif
+    flag_put(true, 0, dec << 1);
     timeout = budget;
     inback = false;
     moves = 0;
@@ -362,7 +382,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       uint32_t byte = 0;
       for (int k = 0; k < 8; ++k) {
         const int d = 8 * j + k;
-        if (d <= frontier && d < T) byte |= (uint32_t)(flags[d * kFanoThreads + lane] >> 1) << (7 - k);
+        if (d <= frontier && d < T) byte |= (flag_get(d) >> 1) << (7 - k);
       }
       a.out[(size_t)b * OB + j] = (uint8_t)byte;
       if (a.info && j < IB) {
@@ -401,10 +421,10 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     // everything a backward move can read, fetched before the move is decided
     const int cm = cur > 0 ? cur - 1 : 0;
     const MT mprev = metric[cm * kFanoThreads + lane];
-    const uint32_t fprev = flags[cm * kFanoThreads + lane];
-    const uint32_t fold = flags[(cur >= K ? cur - K : 0) * kFanoThreads + lane];
+    const uint32_t fprev = flag_get(cm);
+    const uint32_t fold = flag_get(cur >= K ? cur - K : 0);
     FanoRow<HARD, NP> rowm{}, rowp{};
-    if constexpr (ROWS && !WIN) {
+    if constexpr (ROWS) {
       rowm = row_at(cm);
       rowp = row_at(cur + 1 < T ? cur + 1 : T - 1);
     }
@@ -449,24 +469,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       continue;
     }
     metric[(fwd ? ncur : T) * kFanoThreads + lane] = ms;
-    if constexpr (WIN) {
-      // the previous pass's load lands here, one pass after it was issued
-      FanoRow<HARD, NP> ea = rwa, eb = rwb;
-      ea.pick(pdir < 0, rwn, false, rwn);
-      eb.pick(pdir > 0, rwn, false, rwn);
-      const FanoRow<HARD, NP> old0 = row0;
-      row0.pick(fwd, eb, bstep, ea);
-      rwa = ea;
-      rwa.pick(fwd, old0, false, old0);
-      rwb = eb;
-      rwb.pick(bstep, old0, false, old0);
-      // the row beyond the new edge (clamped into the block: never read when clamped)
-      const int edge = fwd ? (ncur + 1 < T ? ncur + 1 : T - 1) : (ncur > 0 ? ncur - 1 : 0);
-      rwn = row_at(edge);
-      pdir = fwd ? 1 : (bstep ? -1 : 0);
-    } else if constexpr (ROWS) {
-      row0.pick(fwd, rowp, bstep, rowm);
-    }
+    if constexpr (ROWS) row0.pick(fwd, rowp, bstep, rowm);
     MT n0, n1;
     uint32_t sw;
     node_metrics(rx, ncur, st, row0, n0, n1, sw);
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     tm1 = need ? n1 : tm1;
     dec = fwd ? sw : dec;
     const bool wflag = fwd || flip || (bstep && untried);
-    flags[(wflag ? ncur : T) * kFanoThreads + lane] = (uint8_t)((bstep ? 1u : 0u) | (dec << 1));
+    flag_put(wflag, ncur, (bstep ? 1u : 0u) | (dec << 1));
   }
   }
   if (a.stats) {   // all lanes again (those without a block skipped the loop)

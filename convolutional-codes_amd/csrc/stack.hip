@@ -148,7 +148,6 @@ static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
 template <bool HARD>
 static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream_t s) {
   if (a.K <= 32 && a.n == 2) {
-    if (rm == kRowsWindow) return launch_fano_v<HARD, 2, true, kRowsWindow>(a, lds, s);
     if (rm == kRowsLds) return launch_fano_v<HARD, 2, true, kRowsLds>(a, lds, s);
     if (rm == kRowsGlobal) return launch_fano_v<HARD, 2, true, kRowsGlobal>(a, lds, s);
     return launch_fano_v<HARD, 2, true, kRowsDirect>(a, lds, s);
@@ -172,14 +171,16 @@ static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream
 // (16 B per node) cut the chip from 9 to 2 waves per CU and run 4x slower. The plan option
 // "fano_rows" (FanoArgs::rows_mode) overrides.
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
-  const size_t node_bytes = ((size_t)(a.T + 1) * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1) + 15) & ~(size_t)15;
+  if (CCV_FANO_FLAGREG && a.T + 1 > 64) return hipErrorInvalidValue;   // the flag masks hold 64 nodes
+  const size_t node_bytes =
+      ((size_t)(a.T + 1) * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + fano_flag_bytes_per_node()) + 15) &
+      ~(size_t)15;
   const size_t row_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : 16);
   const bool rowable = hard || (a.n == 2 && a.K <= 32);
   int rm = hard ? kRowsLds : (rowable ? kRowsGlobal : kRowsDirect);
   if (a.rows_mode >= 0) rm = rowable ? a.rows_mode : kRowsDirect;
   if (rm == kRowsLds && node_bytes + row_bytes > 80 * 1024) rm = kRowsGlobal;
-  if (rm == kRowsWindow && !(a.n == 2 && a.K <= 32)) rm = kRowsGlobal;
-  if (rm < 0 || rm > 3) rm = kRowsDirect;
+  if (rm < 0 || rm > 2) rm = kRowsDirect;
   const size_t lds = node_bytes + (rm == kRowsLds ? row_bytes : 0);
   return hard ? launch_fano_h<true>(a, rm, lds, s) : launch_fano_h<false>(a, rm, lds, s);
 }

@@ -191,7 +191,7 @@ int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out
  *                 "stack_keys"       1 packed metric / index keys for hard input where they fit (default), 0
  *                 "stack_symtab"     1 expected-symbol table (default), 0 parities per iteration
  *   Fano plans:   "fano_rows"        -1 auto (default: 1 hard, 2 soft r = 1/2), 0 read after the move,
- *                                    1 LDS, 2 both candidates prefetched, 3 register window
+ *                                    1 LDS, 2 both candidates prefetched
  *                 "fano_symtab"      -1 auto (table for hard input), 0, 1
  *                 "fano_order"       1 noisiest blocks first for soft input (default), 0 natural order
  *                 "fano_cap"         -1 default (4000 x T moves), 0 one pass, else moves before parking

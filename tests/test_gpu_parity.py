@@ -980,8 +980,8 @@ def test_plan_options_validate(torch_cuda):
             plan.set_option(name, value)
     with pytest.raises(Exception, match="8 or 16"):
         StackPlan(K15, HARD).set_option("stack_row_lanes", 4)
-    with pytest.raises(Exception, match="0..3"):
-        FanoPlan(K15, SOFT).set_option("fano_rows", 4)
+    with pytest.raises(Exception, match="0..2"):
+        FanoPlan(K15, SOFT).set_option("fano_rows", 3)
 
 
 def test_device_channel_rejects_huge_noise(torch_cuda):

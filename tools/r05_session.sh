@@ -77,4 +77,24 @@ phase_b() {
   mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
 }
 
+# c: the whole GPU suite on the options / pruning tree; the fp32-metric BSC kernel (parity + A/B
+# against u16 and the two-popcount branch metrics); Fano flags in registers (parity + A/B); the
+# headline with the non-temporal HBM probe.
+phase_c() {
+  O=gpurun_out/r05c; mkdir -p $O
+  timeout -k 10 900 $PYT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+  echo "gpu suite: $(tail -n 1 $O/pytest_gpu.log)"
+  CCV_LIB_DIR=$AB/hflt/lib timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "hard or bsc or persist or golden" \
+      > $O/pytest_hflt.log 2>&1 || { tail -30 $O/pytest_hflt.log; exit 1; }
+  echo "hflt parity: $(tail -n 1 $O/pytest_hflt.log)"
+  CCV_LIB_DIR=$AB/flagreg/lib timeout -k 10 600 $PYT tests/test_gpu_fano.py > $O/pytest_flagreg.log 2>&1 \
+      || { tail -30 $O/pytest_flagreg.log; exit 1; }
+  echo "flagreg parity: $(tail -n 1 $O/pytest_flagreg.log)"
+  timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_k7.log 2>&1; show $O/bench_k7.log
+  REPS=3 TAG=bsc2 tools/ab_bench.sh "--channel bsc" head hbm hflt
+  REPS=2 TAG=fanoreg tools/ab_bench.sh "--decoder fano --steps 3 --warmup 1" head flagreg
+  REPS=2 TAG=fanoregbsc tools/ab_bench.sh "--decoder fano --channel bsc --steps 3 --warmup 1" head flagreg
+  mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
+}
+
 "phase_$1"
