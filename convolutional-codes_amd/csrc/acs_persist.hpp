@@ -428,24 +428,17 @@ __device__ __forceinline__ uint32_t lds_read_u8(uint32_t addr) {
   return r;
 }
 
-// Round-5 A/B switches (build time): per-step scheduling barrier, branch metrics from two
-// popcounts, the next chunk's symbols read one chunk ahead.
-#ifndef CCV_HARD_SCHED_BARRIER
-#define CCV_HARD_SCHED_BARRIER 1
-#endif
-#ifndef CCV_HARD_BM_PAIRS
-#define CCV_HARD_BM_PAIRS 0
-#endif
-#ifndef CCV_HARD_SYM_AHEAD
-#define CCV_HARD_SYM_AHEAD 0
-#endif
-// metric type of the BSC persistent kernel: 2 = uint16_t (v_add_u16 / v_min_u16), 3 = fp32 (exact for
-// these small integer metrics: the soft kernel's v_add_f32 / v_min_f32 / v_sub_f32 stream)
-#ifndef CCV_HARD_MMODE
-#define CCV_HARD_MMODE 2
-#endif
-
-template <CodeSpec C, int BLEN, int MMODE = CCV_HARD_MMODE>
+// Metric type of the BSC persistent kernel (MMODE): 3 = fp32 (production since round 5), 2 = uint16_t
+// (v_add_u16 / v_min_u16, rounds 2-4), 1 = u32, 0 = inline-asm u16 (ablations, tools/persist_bench).
+// Every metric of this kernel is a small integer (<= n * T after the growth steps, whose unreachable
+// states hold the constant 0xFF00), so fp32 adds, mins and the sign of m1 - m0 are exact and give the
+// u16 decisions and path metrics bit for bit -- and the instruction stream is the soft kernel's
+// (v_add_f32 / v_min_f32 / v_sub_f32 / v_alignbit). The u16 stream's waves were issue-stalled 0.33 of
+// their lifetime (round-4 PMC) against 0.12 for the soft kernel: fp32 runs 0.428 instead of 0.456 ms per
+// 104-frame launch, 239 instead of 225 Gbit/s (profiles/r05c/ab/bsc2_*). Also measured in round 5
+// (profiles/r05a/ab/bsc_*, u16): no scheduling barrier between steps, the next chunk's symbols read a
+// chunk ahead, two popcounts for the four branch metrics -- all within +-0.8 %.
+template <CodeSpec C, int BLEN, int MMODE = 3>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void viterbi_hard_persist(RegArgs a, int ngroups) {
   constexpr int S = 1 << (C.K - 1);
@@ -500,13 +493,10 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
     if (g + stride_groups < ngroups) issue_group(g + stride_groups, buf ^ 1);
     const uint32_t row_addr = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * kBuf + lane * T);
     const uint64_t info = load_info<BLEN>(a, b);
-    // metric type: 2 = plain uint16_t (production: v_add_u16 / v_min_u16, full rate, visible to the
-    // scheduler); 0 = H16 inline-asm ops (round 2 first cut: hipcc puts an s_nop 0 after every
-    // inline-asm VALU whose result is read next, 1,612 per group, 6 % slower); 1 = u32 (v_bcnt-folded
-    // adds and v_min_u32, half rate: 25 % slower). tools/persist_bench abh.
-    //  3 = fp32: every metric here is a small integer (<= n * T < 2^24 after the growth steps, the
-    //  unreachable growth states the constant 0xFF00), so fp32 adds, mins and the sign of m1 - m0 are
-    //  exact and give the u16 decisions bit for bit.
+    // metric type (see above): 3 = fp32 (production); 2 = plain uint16_t (v_add_u16 / v_min_u16,
+    // rounds 2-4); 0 = H16 inline-asm ops (round 2 first cut: hipcc puts an s_nop 0 after every
+    // inline-asm VALU whose result is read next, 6 % slower than 2); 1 = u32 (v_bcnt-folded adds and
+    // v_min_u32, half rate: 25 % slower than 2). tools/persist_bench abh.
     using MT = typename std::conditional<
         MMODE == 3, float,
         typename std::conditional<MMODE == 1, uint32_t,
@@ -515,31 +505,17 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
 #pragma unroll
     for (int s = 0; s < S; ++s) M[s] = MT{(MT)(s ? 0xFF00u : 0u)};   // viterbi-decoder.c:225-228
     DW D[BLEN];
-    constexpr bool AHEAD = CCV_HARD_SYM_AHEAD != 0;
-    uint32_t symq[2][PF];   // AHEAD: chunk c's symbols in symq[c & 1], chunk c + 1's in flight
-    if constexpr (AHEAD) {
-      [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
-        ((symq[0][us] = lds_read_u8<us>(row_addr)), ...);
-      }(std::make_integer_sequence<int, PF>{});
-    }
     auto chunk_at = [&]<int c>() __attribute__((always_inline)) {
       if (c * PF >= a.T) return;   // always true: per-chunk basic blocks (see the soft kernel)
       // inline-asm LDS reads: the compiler would otherwise wait for the NEXT group's DMA (into the
       // other buffer) before every read, since it cannot tell the buffers apart
-      uint32_t* sym = AHEAD ? symq[c & 1] : symq[0];
-      if constexpr (!AHEAD) {
-        [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
-          ((sym[us] = lds_read_u8<c * PF + us>(row_addr)), ...);
-        }(std::make_integer_sequence<int, PF>{});
-      }
+      uint32_t sym[PF];
+      [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
+        ((sym[us] = lds_read_u8<c * PF + us>(row_addr)), ...);
+      }(std::make_integer_sequence<int, PF>{});
       asm volatile("s_waitcnt lgkmcnt(0)"
                    : "+v"(sym[0]), "+v"(sym[1]), "+v"(sym[2]), "+v"(sym[3]), "+v"(sym[4]), "+v"(sym[5]),
                      "+v"(sym[6]), "+v"(sym[7]));
-      if constexpr (AHEAD && c + 1 < NCH) {
-        [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {
-          ((symq[(c + 1) & 1][us] = lds_read_u8<(c + 1) * PF + us>(row_addr)), ...);
-        }(std::make_integer_sequence<int, PF>{});
-      }
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
         constexpr int t = c * PF + u;
         if constexpr (t < T) {
@@ -552,14 +528,6 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
             BM[1] = p1;
             BM[2] = 2.0f - p1;
             BM[3] = 2.0f - p0;
-          } else if constexpr (CCV_HARD_BM_PAIRS != 0 && NS == 4) {
-            // popcount(k ^ s) over n = 2 bits: k and k ^ 3 sum to 2
-            const uint32_t p0 = (uint32_t)__builtin_popcount(sym[u] & kMask);
-            const uint32_t p1 = (uint32_t)__builtin_popcount((sym[u] ^ 1u) & kMask);
-            BM[0] = (MT)p0;
-            BM[1] = (MT)p1;
-            BM[2] = (MT)(2u - p1);
-            BM[3] = (MT)(2u - p0);
           } else {
 #pragma unroll
             for (int k = 0; k < NS; ++k) BM[k] = MT{(MT)__builtin_popcount((uint32_t)k ^ (sym[u] & kMask))};
@@ -573,7 +541,7 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
             D[t - G] = acs_step<C, false, MT>(M, BM);
             pin(D[t - G]);
           }
-          if constexpr (CCV_HARD_SCHED_BARRIER != 0) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
         }
       };
       [&]<int... us>(std::integer_sequence<int, us...>) __attribute__((always_inline)) {

@@ -444,6 +444,9 @@ __device__ __forceinline__ uint32_t traceback_lds(const RegArgs& a, const DW* co
   return owner ? errors : 0u;
 }
 
+#ifndef CCV_CHANNEL_HARD_U16
+#define CCV_CHANNEL_HARD_U16 0
+#endif
 template <CodeSpec C, bool HARD>
 __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   constexpr int S = 1 << (C.K - 1);
@@ -452,7 +455,9 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   using DW = DecWord<S>;
   using Src = ChannelSource<C, HARD>;
   using SM = typename Src::MT;                                      // source metric type
-  using MT = typename std::conditional<HARD, uint16_t, float>::type;   // ACS metric type
+  // ACS metric type: fp32 for both channels (BSC metrics are small integers, exact in fp32: the
+  // persistent BSC kernel's round-5 change, acs_persist.hpp); CCV_CHANNEL_HARD_U16=1 keeps uint16_t
+  using MT = typename std::conditional<HARD && CCV_CHANNEL_HARD_U16, uint16_t, float>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char chan_lds[];
   DW* dl = reinterpret_cast<DW*>(chan_lds);
   const int lane = threadIdx.x;
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       BM[k] = (MT)raw[k];
-      if constexpr (HARD) asm volatile("" : "+v"(BM[k]));   // no v_bcnt-folded adds (acs_reg.hpp)
+      if constexpr (std::is_same_v<MT, uint16_t>) asm volatile("" : "+v"(BM[k]));   // no v_bcnt-folded adds (acs_reg.hpp)
     }
   };
   // T >= K > G: every block has its K-1 growth steps
@@ -491,7 +496,7 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
     dl[(size_t)(t - G) * kRegThreads + lane] = acs_step<C, false, MT>(M, BM);
   }
   // each lane reads back only its own column: no barrier
-  using AM = typename std::conditional<HARD, uint32_t, float>::type;
+  using AM = typename std::conditional<std::is_same_v<MT, uint16_t>, uint32_t, float>::type;
   AM Ma[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) Ma[s] = (AM)M[s];

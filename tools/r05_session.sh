@@ -97,4 +97,37 @@ phase_c() {
   mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
 }
 
+# c2: the A/B part of c (its tests passed: 586 + 1 xfail, hflt 172; flagreg fails by design where
+# T + 1 > 64)
+phase_c2() {
+  O=gpurun_out/r05c; mkdir -p $O
+  timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_k7.log 2>&1; show $O/bench_k7.log
+  REPS=3 TAG=bsc2 tools/ab_bench.sh "--channel bsc" head hbm hflt
+  REPS=2 TAG=fanoreg tools/ab_bench.sh "--decoder fano --steps 3 --warmup 1" head flagreg
+  REPS=2 TAG=fanoregbsc tools/ab_bench.sh "--decoder fano --channel bsc --steps 3 --warmup 1" head flagreg
+  mkdir -p $O/ab && cp gpurun_out/ab/* $O/ab/
+}
+
+# d: the GPU suite with fp32 BSC metrics as the default (persistent and channel kernels); the BSC
+# fused channel + decode against the u16 channel ACS; the PMC passes of the new BSC kernel.
+phase_d() {
+  O=gpurun_out/r05d; mkdir -p $O
+  timeout -k 10 900 $PYT tests -m gpu > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+  echo "gpu suite: $(tail -n 1 $O/pytest_gpu.log)"
+  for rep in 1 2; do
+    for v in head chu16; do
+      dir=$AB/$v/lib; [ $v = head ] && dir=$PWD/convolutional-codes_amd/lib
+      CCV_LIB_DIR=$dir timeout -k 10 300 python bench.py --channel bsc --no-cpu-baseline --no-hbm-probe > $O/bsc_fused_${v}_$rep.log 2>&1 \
+          || { tail -5 $O/bsc_fused_${v}_$rep.log; exit 1; }
+      python3 -c "
+import json; d=json.loads(open('$O/bsc_fused_${v}_$rep.log').read().strip().splitlines()[-1])
+print('bsc $v rep $rep', d['value'], d['kernel_ms'], 'fused', d['fused_channel']['mbit_s'], d['fused_channel']['kernel_ms'])"
+    done
+  done
+  bash tools/pmc_workload.sh --channel bsc > $O/pmc_bsc.log 2>&1 || { tail -20 $O/pmc_bsc.log; exit 1; }
+  timeout -k 10 300 python -m ccviterbi.sim --code k7 --channel bsc --points 20000,50000 --device-channel > $O/sweep_bsc_k7.log 2>&1 \
+      || { tail -5 $O/sweep_bsc_k7.log; exit 1; }
+  grep '^{' $O/sweep_bsc_k7.log | cut -c1-300
+}
+
 "phase_$1"
