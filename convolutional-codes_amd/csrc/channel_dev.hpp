@@ -444,9 +444,6 @@ __device__ __forceinline__ uint32_t traceback_lds(const RegArgs& a, const DW* co
   return owner ? errors : 0u;
 }
 
-#ifndef CCV_CHANNEL_HARD_U16
-#define CCV_CHANNEL_HARD_U16 0
-#endif
 template <CodeSpec C, bool HARD>
 __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   constexpr int S = 1 << (C.K - 1);
@@ -455,9 +452,10 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   using DW = DecWord<S>;
   using Src = ChannelSource<C, HARD>;
   using SM = typename Src::MT;                                      // source metric type
-  // ACS metric type: fp32 for both channels (BSC metrics are small integers, exact in fp32: the
-  // persistent BSC kernel's round-5 change, acs_persist.hpp); CCV_CHANNEL_HARD_U16=1 keeps uint16_t
-  using MT = typename std::conditional<HARD && CCV_CHANNEL_HARD_U16, uint16_t, float>::type;
+  // ACS metric type: uint16_t for the BSC (fp32, exact here as in the persistent BSC kernel,
+  // acs_persist.hpp, measured 1 % slower in this kernel, whose time is the channel's: 108.7-109.7 vs
+  // 110.1-111.0 Gbit/s with u16, profiles/r05d/)
+  using MT = typename std::conditional<HARD, uint16_t, float>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char chan_lds[];
   DW* dl = reinterpret_cast<DW*>(chan_lds);
   const int lane = threadIdx.x;

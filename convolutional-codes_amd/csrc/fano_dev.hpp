@@ -102,13 +102,9 @@ __global__ void fano_score(const float* in, int T, int nblocks, float* key, uint
 
 constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
 
-// CCV_FANO_FLAGREG (A/B, round 5): a node's flags (selected branch, decoded input) as bits of two
-// 64-bit masks per lane instead of a byte per node in LDS -- the node arrays shrink from 5 to 4 bytes
-// per node, 9 -> 11 waves per CU at K = 15 (T + 1 <= 64 required).
-#ifndef CCV_FANO_FLAGREG
-#define CCV_FANO_FLAGREG 0
-#endif
-__host__ __device__ constexpr size_t fano_flag_bytes_per_node() { return CCV_FANO_FLAGREG ? 0 : 1; }
+// (Round 5 measured and removed a node-flag form with two 64-bit masks per lane instead of a byte
+// per node in LDS: 9 -> 11 waves per CU at K = 15, but the mask updates cost more than the occupancy
+// gained -- 67 -> 60 Mbit/s soft, 222 -> 218 BSC, profiles/r05c/ab/fanoreg*.)
 constexpr int kFanoThreads = 64;
 
 // Received-symbol access per lane (RM):
@@ -165,30 +161,11 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   MT* metric = reinterpret_cast<MT*>(smem);
   uint8_t* flags = smem + (size_t)(T + 1) * kFanoThreads * sizeof(MT);   // sel | dec << 1
   // rows: [T][64] float4 (soft) or bytes (hard), after the flags (16-byte aligned)
-  unsigned char* rows =
-      smem + (((size_t)(T + 1) * kFanoThreads * (sizeof(MT) + fano_flag_bytes_per_node()) + 15) & ~(size_t)15);
-#if CCV_FANO_FLAGREG
-  uint64_t fsel = 0, fdec = 0;   // bit d: node d's selected branch / decoded input
-  (void)flags;
-#endif
-  // a node's flags byte (sel | dec << 1): LDS, or the lane's two masks
-  auto flag_get = [&](int d) -> uint32_t {
-#if CCV_FANO_FLAGREG
-    return (uint32_t)((fsel >> d) & 1u) | ((uint32_t)((fdec >> d) & 1u) << 1);
-#else
-    return flags[d * kFanoThreads + lane];
-#endif
-  };
-  // store v at node d when `write` (otherwise nothing; the LDS form writes the spare row T instead)
-  auto flag_put = [&](bool write, int d, uint32_t v) {
-#if CCV_FANO_FLAGREG
-    const uint64_t m = write ? (1ull << d) : 0ull;
-    fsel = (fsel & ~m) | ((v & 1u) ? m : 0ull);
-    fdec = (fdec & ~m) | ((v & 2u) ? m : 0ull);
-#else
-    flags[(write ? d : T) * kFanoThreads + lane] = (uint8_t)v;
-#endif
-  };
+  unsigned char* rows = smem + (((size_t)(T + 1) * kFanoThreads * (sizeof(MT) + 1) + 15) & ~(size_t)15);
+  // a node's flags byte (sel | dec << 1)
+  auto flag_get = [&](int d) -> uint32_t { return flags[d * kFanoThreads + lane]; };
+  // store v at node d when `write`; otherwise into the spare row T (branch-free)
+  auto flag_put = [&](bool write, int d, uint32_t v) { flags[(write ? d : T) * kFanoThreads + lane] = (uint8_t)v; };
   uint64_t poly[kMaxN];
 #pragma unroll
   for (int k = 0; k < kMaxN; ++k) poly[k] = a.poly[k];
@@ -324,9 +301,6 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     frontier = (int)h[2];
     const MT* pm = static_cast<const MT*>(a.park_metric) + (size_t)slot * (T + 1);
     const uint8_t* pf = a.park_flags + (size_t)slot * (T + 1);
-#if CCV_FANO_FLAGREG
-    fsel = fdec = 0;
-#endif
     for (int d = 0; d <= frontier; ++d) {
       metric[d * kFanoThreads + lane] = pm[d];
       flag_put(true, d, pf[d]);
@@ -366,9 +340,6 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     node_metrics(rx, 0, 0, row0, tm0, tm1, sw);
     sel = 0;
     dec = sw;
-#if CCV_FANO_FLAGREG
-    fsel = fdec = 0;
-#endif
     flag_put(true, 0, dec << 1);
     timeout = budget;
     inback = false;

@@ -351,71 +351,9 @@ __device__ __forceinline__ float vmin2(float a, float b) { float r; asm("v_min_f
 __device__ __forceinline__ int32_t vmax2(int32_t a, int32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ int32_t vmin2(int32_t a, int32_t b) { return a < b ? a : b; }
 
-// The same pair of row reductions through the LDS crossbar (ds_swizzle, bit mode: lane ^ m within 32
-// lanes, m = 1, 2, 4, 8), with no cross-lane VALU instruction -- which on gfx950 drops a wave's whole
-// VALU stream to about half rate for the next ~1000 instructions (tools/raterbench7.hip,
-// profiles/r04c/raterbench7.txt). NOT the default: the stack search is latency-bound, and the
-// swizzles' LDS-unit round trips in the iteration's dependent chain cost more than the halved VALU
-// rate (round 4 A/B: soft 587 -> 445, BSC 1285 -> 1074 Mbit/s). CCV_STACK_SWZ=1 at build time.
-#ifndef CCV_STACK_SWZ
-#define CCV_STACK_SWZ 0
-#endif
-template <int M>
-__device__ __forceinline__ int32_t swz_xor(int32_t v) {
-  return __builtin_amdgcn_ds_swizzle(v, (M << 10) | 0x1F);   // and 0x1F, or 0, xor M
-}
-template <int RL, class F>
-__device__ __forceinline__ void row_pair_swz(uint32_t& a, uint32_t& b, F&& combine) {
-  auto step = [&]<int M>() __attribute__((always_inline)) {
-    const uint32_t ta = (uint32_t)swz_xor<M>((int32_t)a), tb = (uint32_t)swz_xor<M>((int32_t)b);
-    combine(a, b, ta, tb);
-  };
-  step.template operator()<1>();
-  step.template operator()<2>();
-  step.template operator()<4>();
-  if constexpr (RL == 16) step.template operator()<8>();
-}
-template <int RL>
-__device__ __forceinline__ void row_max_min_swz(float& a, float& b) {
-  uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-  row_pair_swz<RL>(ua, ub, [](uint32_t& x, uint32_t& y, uint32_t tx, uint32_t ty) {
-    x = __float_as_uint(vmax2(__uint_as_float(x), __uint_as_float(tx)));
-    y = __float_as_uint(vmin2(__uint_as_float(y), __uint_as_float(ty)));
-  });
-  a = __uint_as_float(ua);
-  b = __uint_as_float(ub);
-}
-template <int RL>
-__device__ __forceinline__ void row_max_min_swz(int32_t& a, int32_t& b) {
-  uint32_t ua = (uint32_t)a, ub = (uint32_t)b;
-  row_pair_swz<RL>(ua, ub, [](uint32_t& x, uint32_t& y, uint32_t tx, uint32_t ty) {
-    x = (uint32_t)vmax2((int32_t)x, (int32_t)tx);
-    y = (uint32_t)vmin2((int32_t)y, (int32_t)ty);
-  });
-  a = (int32_t)ua;
-  b = (int32_t)ub;
-}
-template <int RL>
-__device__ __forceinline__ void row_min_min_u32_swz(uint32_t& a, uint32_t& b) {
-  row_pair_swz<RL>(a, b, [](uint32_t& x, uint32_t& y, uint32_t tx, uint32_t ty) {
-    x = tx < x ? tx : x;
-    y = ty < y ? ty : y;
-  });
-}
-
 // LDS bytes per row: the block's symbols (16-byte aligned), 65 entry records (64 + a dummy), then
 // the 64 path metrics + the dummy (padded to 68)
-// CCV_STACK_SYMG=1 (A/B, soft input): the rows kernel reads the block's demapped symbols from global
-// memory (L2) instead of staging them in LDS -- 864 fewer LDS bytes per K = 15 search, so more
-// resident waves, against a cache round trip in the iteration's chain
-#ifndef CCV_STACK_SYMG
-#define CCV_STACK_SYMG 0
-#endif
-#ifndef CCV_STACK_SGPR_SEL
-#define CCV_STACK_SGPR_SEL 0
-#endif
 __host__ __device__ constexpr size_t stack_rows_sym_bytes(int T, int ns, bool hard) {
-  if (CCV_STACK_SYMG && !hard) return 0;
   return (((size_t)T * (size_t)ns * (hard ? 1 : 4)) + 15) & ~(size_t)15;
 }
 __host__ __device__ constexpr size_t stack_rows_row_bytes(int T, int ns, bool hard) {
@@ -493,17 +431,12 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
     return __shfl((int)b, rbase, 64);
   };
   // stage a block's symbols and the root entry; the row's LDS is private to its 16 lanes
-  constexpr bool kSymG = CCV_STACK_SYMG && !HARD;
-  const ET* gsyms = in;
   auto stage = [&](int b) {
     const ET* src = in + (size_t)b * per;
-    gsyms = src;
-    if constexpr (!kSymG) {
-      for (int i = l; i < per; i += kRowLanes) {
-        ET v = src[i];
-        if constexpr (HARD) v = (ET)(v & symmask);   // binary-symmetric-channel/stack-decoder.c:116-118
-        syms[i] = v;
-      }
+    for (int i = l; i < per; i += kRowLanes) {
+      ET v = src[i];
+      if constexpr (HARD) v = (ET)(v & symmask);   // binary-symmetric-channel/stack-decoder.c:116-118
+      syms[i] = v;
     }
     if (l == 0) ent[0] = make_uint4(esym_root << 8, 0u, 0u, 0u);
 #pragma unroll
@@ -535,8 +468,7 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
           kx = vmax2(kx, (int32_t)((uint32_t)met[k] * 64u) + (63 - (l * kRowSlots + k)));
           kn = vmin2(kn, (int32_t)((uint32_t)met[k] * 64u) + (l * kRowSlots + k));
         }
-        if constexpr (CCV_STACK_SWZ) row_max_min_swz<RL>(kx, kn);
-        else row_max_min<RL>(kx, kn);
+        row_max_min<RL>(kx, kn);
         mx = (MT)(kx >> 6);
         cur = 63u - ((uint32_t)kx & 63u);
         ok = kx > -(1 << 30);
@@ -550,54 +482,15 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
           mx = vmax2(mx, met[k]);
           mn = vmin2(mn, met[k]);
         }
-        if constexpr (CCV_STACK_SWZ) row_max_min_swz<RL>(mx, mn);
-        else row_max_min<RL>(mx, mn);
+        row_max_min<RL>(mx, mn);
         uint32_t cand = kStackDepth;
         c2 = kStackDepth;
-        if constexpr (CCV_STACK_SGPR_SEL && kRowSlots == 4 && !HARD) {
-          // the eight compares into SGPR pairs first, then the selects: hipcc's form is a serial
-          // v_cmp -> VCC -> v_cndmask_e32 chain with an s_nop 1 in each link (2 wait states after a
-          // VALU SGPR write on gfx950), and a VCC compare/select pair costs ~7 ns per instruction
-          // (profiles/r02_rates_argmin.txt). Here every select reads a mask written >= 2 VALU
-          // instructions earlier: no wait state, no VCC. Same result: the lowest k with
-          // met[k] == mx (resp. mn) wins. Float metrics only (the compare is v_cmp_eq_f32).
-          const uint32_t i0 = (uint32_t)(l * kRowSlots);
-          uint64_t e0, e1, e2, e3, f0, f1, f2, f3;
-          uint32_t tmp;
-          asm volatile(
-              "v_cmp_eq_f32_e64 %[e3], %[m3], %[mx]\n"
-              "v_cmp_eq_f32_e64 %[f3], %[m3], %[mn]\n"
-              "v_cmp_eq_f32_e64 %[e2], %[m2], %[mx]\n"
-              "v_cmp_eq_f32_e64 %[f2], %[m2], %[mn]\n"
-              "v_cmp_eq_f32_e64 %[e1], %[m1], %[mx]\n"
-              "v_cmp_eq_f32_e64 %[f1], %[m1], %[mn]\n"
-              "v_cmp_eq_f32_e64 %[e0], %[m0], %[mx]\n"
-              "v_cmp_eq_f32_e64 %[f0], %[m0], %[mn]\n"
-              "v_add_u32 %[t], 3, %[i0]\n"
-              "v_cndmask_b32_e64 %[c], 64, %[t], %[e3]\n"
-              "v_cndmask_b32_e64 %[d], 64, %[t], %[f3]\n"
-              "v_add_u32 %[t], 2, %[i0]\n"
-              "v_cndmask_b32_e64 %[c], %[c], %[t], %[e2]\n"
-              "v_cndmask_b32_e64 %[d], %[d], %[t], %[f2]\n"
-              "v_add_u32 %[t], 1, %[i0]\n"
-              "v_cndmask_b32_e64 %[c], %[c], %[t], %[e1]\n"
-              "v_cndmask_b32_e64 %[d], %[d], %[t], %[f1]\n"
-              "v_cndmask_b32_e64 %[c], %[c], %[i0], %[e0]\n"
-              "v_cndmask_b32_e64 %[d], %[d], %[i0], %[f0]\n"
-              : [e0] "=&s"(e0), [e1] "=&s"(e1), [e2] "=&s"(e2), [e3] "=&s"(e3), [f0] "=&s"(f0),
-                [f1] "=&s"(f1), [f2] "=&s"(f2), [f3] "=&s"(f3), [c] "=&v"(cand), [d] "=&v"(c2),
-                [t] "=&v"(tmp)
-              : [m0] "v"(met[0]), [m1] "v"(met[1]), [m2] "v"(met[2]), [m3] "v"(met[3]), [mx] "v"(mx),
-                [mn] "v"(mn), [i0] "v"(i0));
-        } else {
 #pragma unroll
-          for (int k = kRowSlots - 1; k >= 0; --k) {
-            cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
-            c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
-          }
+        for (int k = kRowSlots - 1; k >= 0; --k) {
+          cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
+          c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
         }
-        if constexpr (CCV_STACK_SWZ) row_min_min_u32_swz<RL>(cand, c2);
-        else row_min_min_u32<RL>(cand, c2);
+        row_min_min_u32<RL>(cand, c2);
         cur = cand;
         ok = mx > lo_sent;
       }
@@ -621,7 +514,6 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       uint32_t es = symbols_of(est);
       ET r0, r1;
       if constexpr (HARD) { r0 = r1 = syms[ci]; }
-      else if constexpr (kSymG) { r0 = gsyms[ci * NS + e0]; r1 = gsyms[ci * NS + e1]; }
       else { r0 = syms[ci * NS + e0]; r1 = syms[ci * NS + e1]; }
       if (ext && c_next >= (uint32_t)tn) {
         // symbols at or beyond the frontier are still the previous block's (header of stack_decode)

@@ -85,7 +85,7 @@ def main():
         "raw_fetch_bytes_per_launch": d_fetch, "raw_write_bytes_per_launch": d_write,
         "calibration": {"copy_kernel": copy_k[0], "copy_bytes": copy_bytes, "read_scale": read_scale,
                         "write_scale": write_scale},
-        "source": os.path.relpath(root) + " (committed as profiles/r03_pmc/<tag>_{FETCH,WRITE,SQ,STALL}.csv)",
+        "source": os.path.relpath(root) + " (committed as profiles/r05_pmc/<tag>_{FETCH,WRITE,SQ,STALL}.csv)",
     }
     for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_BUSY_CYCLES",
               "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"):
