@@ -404,12 +404,14 @@ def main(argv=None):
     if hard and args.layout != "block":
         raise SystemExit("hard-decision input is one byte per step, block-major")
     chan = HARD if hard else SOFT
+    t_prod = time.perf_counter()
     if hard:
         info, rx = ch.bsc_blocks(code, nb, args.p_ppm, args.seed, first_block=rank * nb,
                                  threads=cpu_threads())
     else:
         info, rx = ch.awgn_blocks(code, nb, ch.noise_scaling(args.ebn0), args.seed, first_block=rank * nb,
                                   threads=cpu_threads())
+    t_prod = time.perf_counter() - t_prod
     host_in = rx if args.layout == "block" else np.ascontiguousarray(rx.transpose(1, 0, 2))
     d_rx = torch.from_numpy(host_in).to("cuda")
     d_info = torch.from_numpy(info).to("cuda")
@@ -594,6 +596,12 @@ def main(argv=None):
             "kernel_ms_median": round(kernel_ms_median, 4),
             "per_rank_kernel_ms": per_rank_kernel_ms,
             "clock_warmup_s": args.clock_warmup,
+            # per rank, before the timed region: the host producer (Philox channel on cpu_threads()
+            # threads) and the host bytes it holds (frames + info; rank 0 adds a pinned copy of the
+            # frames for the PCIe-inclusive rate)
+            "host_producer_s": round(t_prod, 3),
+            "host_producer_threads": cpu_threads(),
+            "host_bytes_per_rank": int(rx.nbytes + info.nbytes),
             "pcie_inclusive_mbit_s": round(nb * code.blen / pcie_s / 1e6, 1) if pcie_s else None,
             "roofline": {
                 "bound": bound,

@@ -24,6 +24,7 @@ FLAG_NO_PERSISTENT = 8      # skip the persistent K <= 7 kernels (A/B)
 
 CHANNEL_HARD_DEMAP = 1     # include/ccv.h CCV_CHANNEL_HARD_DEMAP
 CHANNEL_FRAMES_ONLY = 2    # include/ccv.h CCV_CHANNEL_FRAMES_ONLY
+CHANNEL_NOISE_F32 = 4      # include/ccv.h CCV_CHANNEL_NOISE_F32 (opt-in fp32 Box-Muller)
 
 
 class DecoderError(RuntimeError):
@@ -120,12 +121,15 @@ class Plan:
             raise DecoderError(f"ccv_decode_device: {_native.last_error()}")
 
     def simulate_device(self, seed, first_block, nblocks, channel_param, d_errors=None, d_info=None,
-                        d_out=None, d_path_metric=None, d_channel=None, stream=None, hard_demap=False):
+                        d_out=None, d_path_metric=None, d_channel=None, stream=None, hard_demap=False,
+                        noise_f32=False):
         """On-device channel + decode (ccv_simulate_device): blocks first_block.. of the Philox stream
         `seed`; channel_param = AWGN noise scaling (soft plan) or BSC p_ppm (hard plan); hard_demap
-        selects the reference's hard demapper (common/hard-demapper.c)."""
+        selects the reference's hard demapper (common/hard-demapper.c); noise_f32 the opt-in fp32
+        Box-Muller (statistically, not bit-, equal to the double-precision default)."""
+        flags = (CHANNEL_HARD_DEMAP if hard_demap else 0) | (CHANNEL_NOISE_F32 if noise_f32 else 0)
         rc = self._lib.ccv_simulate_device(self._h, int(seed), int(first_block), int(nblocks),
-                                           float(channel_param), 1 if hard_demap else 0,
+                                           float(channel_param), flags,
                                            _ptr(d_info), _ptr(d_out),
                                            _ptr(d_path_metric), _ptr(d_errors), _ptr(d_channel),
                                            _stream_handle(stream))
@@ -133,11 +137,12 @@ class Plan:
             raise DecoderError(f"ccv_simulate_device: {_native.last_error()}")
 
     def simulate_frames(self, seed, first_block, nblocks, channel_param, d_channel, d_info=None,
-                        stream=None, hard_demap=False):
+                        stream=None, hard_demap=False, noise_f32=False):
         """The on-device channel's frames only (ccv_simulate_device with CCV_CHANNEL_FRAMES_ONLY):
         info bytes into d_info and the decoder input into d_channel, no decode; any plan (Viterbi,
         stack, Fano), any code with n <= 3."""
-        flags = CHANNEL_FRAMES_ONLY | (CHANNEL_HARD_DEMAP if hard_demap else 0)
+        flags = (CHANNEL_FRAMES_ONLY | (CHANNEL_HARD_DEMAP if hard_demap else 0) |
+                 (CHANNEL_NOISE_F32 if noise_f32 else 0))
         rc = self._lib.ccv_simulate_device(self._h, int(seed), int(first_block), int(nblocks),
                                            float(channel_param), flags, _ptr(d_info), None, None, None,
                                            _ptr(d_channel), _stream_handle(stream))

@@ -106,7 +106,8 @@ class DeviceChannelDecoder:
     no Viterbi plan and no decode of the chunk beside the sequential one)."""
 
     def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None,
-                 hard_demap=False, decoder: str = "viterbi", chunk_blocks: Optional[int] = None):
+                 hard_demap=False, decoder: str = "viterbi", chunk_blocks: Optional[int] = None,
+                 noise_f32: bool = False):
         import torch
 
         from .decoder import Plan
@@ -125,6 +126,7 @@ class DeviceChannelDecoder:
         self.plan.reserve(self.chunk)
         self.channel, self.frame_blocks, self.seed = channel, frame_blocks, seed
         self.hard_demap = hard_demap
+        self.noise_f32 = noise_f32
         self.d_err = torch.zeros(1, dtype=torch.int64, device=self.device)
         if self.seq is not None:
             self.seq.reserve(self.chunk)
@@ -163,10 +165,10 @@ class DeviceChannelDecoder:
             nb = min(self.chunk, first_block + nblocks - first)
             if self.seq is None:
                 self.plan.simulate_device(self.seed, first, nb, param, d_errors=self.d_err,
-                                          stream=stream, hard_demap=self.hard_demap)
+                                          stream=stream, hard_demap=self.hard_demap, noise_f32=self.noise_f32)
                 continue
             self.seq.simulate_frames(self.seed, first, nb, param, self.d_ch, d_info=self.d_info,
-                                     stream=stream, hard_demap=self.hard_demap)
+                                     stream=stream, hard_demap=self.hard_demap, noise_f32=self.noise_f32)
             self.seq.decode_device(self.d_ch, nb, self.d_out,
                                    d_path_metric=self.d_pm if self.channel == HARD else None,
                                    d_info=self.d_info, d_errors=self.d_err, stream=stream)
@@ -184,7 +186,7 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
               seed: int = 0xC0DE, rank: int = 0, world: int = 1,
               decode: Optional[Callable[[np.ndarray, np.ndarray], int]] = None,
               threads: Optional[int] = None, reduce: bool = True,
-              device_channel: bool = False, hard_demap: bool = False,
+              device_channel: bool = False, hard_demap: bool = False, noise_f32: bool = False,
               decoder: str = "viterbi", point_index: int = 0,
               device_decoder: Optional["DeviceChannelDecoder"] = None) -> List[BerPoint]:
     """BER at each point; `decode(info, data) -> errors` defaults to the GPU decoder. With
@@ -198,7 +200,10 @@ def ber_sweep(code: Code, points: Sequence[float], channel: int = SOFT,
             bits_per_point = lambda p: reference_bsc_bits(int(p), code.blen)  # noqa: E731
     dev = device_decoder
     if dev is None and device_channel and decode is None:
-        dev = DeviceChannelDecoder(code, channel, frame_blocks, seed, hard_demap=hard_demap, decoder=decoder)
+        dev = DeviceChannelDecoder(code, channel, frame_blocks, seed, hard_demap=hard_demap, decoder=decoder,
+                                   noise_f32=noise_f32)
+    if noise_f32 and dev is None:
+        raise ValueError("noise_f32 is an option of the on-device channel (device_channel=True)")
     if decode is None and dev is None:
         decode = GpuFrameDecoder(code, channel, frame_blocks, decoder=decoder)
     counters = np.zeros((len(points), 2), np.int64)
@@ -297,6 +302,10 @@ def main(argv=None, decode=None):
     ap.add_argument("--device-channel", action="store_true",
                     help="generate the frames on the GPU (encoder, mapper, Philox AWGN / BSC, demapper)")
     ap.add_argument("--hard-demap", action="store_true", help="common/hard-demapper.c instead of demapper.c")
+    ap.add_argument("--noise", choices=("f64", "f32"), default="f64",
+                    help="on-device AWGN Box-Muller: f64 (default, the reference's double precision) or the "
+                         "opt-in f32 from the hardware transcendentals (faster; the same BER statistics, "
+                         "not the same samples)")
     ap.add_argument("--threads", type=int, default=None, help="host producer threads per rank")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); self-launches torchrun")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
@@ -320,6 +329,8 @@ def main(argv=None, decode=None):
     channel = HARD if args.channel == "bsc" else SOFT
     if args.hard_demap and channel != SOFT:
         raise SystemExit("--hard-demap belongs to the AWGN channel")
+    if args.noise == "f32" and (channel != SOFT or not args.device_channel):
+        raise SystemExit("--noise f32 is an option of the on-device AWGN channel (--device-channel)")
     points = _parse_points(args.points, channel)
     backend = args.backend or ("gloo" if decode is not None else "nccl")
 
@@ -346,7 +357,8 @@ def main(argv=None, decode=None):
     if decode is None:
         if args.device_channel:
             dev = DeviceChannelDecoder(code, channel, args.frame_blocks, args.seed,
-                                       hard_demap=args.hard_demap, decoder=args.decoder)
+                                       hard_demap=args.hard_demap, decoder=args.decoder,
+                                       noise_f32=args.noise == "f32")
             if args.warmup > 0:
                 dev.warm_up(args.warmup, points[0] if points else None)
         else:
@@ -376,6 +388,7 @@ def main(argv=None, decode=None):
         rec = {"code": code.name or args.code, "n": code.n, "K": code.K, "blen": code.blen,
                "generator": "ref-x86" if code.gen_mode == 0 else "true-parity",
                "channel": args.channel + ("-hard-demap" if args.hard_demap else ""),
+               "noise": args.noise if channel == SOFT else None,
                "decoder": args.decoder, ("ebn0_db" if channel == SOFT else "p_ppm"): p,
                "errors": errors, "bits": bits, "ber": errors / bits if bits else None,
                "ber_99.9_binomial": [lo, hi], "seconds": round(float(secs[k]), 4),

@@ -50,7 +50,32 @@ struct ChanArgs {
   uint8_t* info_out;         // [nb][IB] transmitted info bytes (required)
   void* ch_out;              // optional export: soft float [nb][T][2^n] / hard uint8 [nb][T]
   int global_decisions;      // K <= 7: decisions through r.dec in HBM instead of LDS (A/B, long T)
+  int noise_f32;             // AWGN: the fp32 Box-Muller (CCV_CHANNEL_NOISE_F32, opt-in) instead of double
 };
+
+// The opt-in fp32 Box-Muller (CCV_CHANNEL_NOISE_F32): the same uniforms k1, k2 / (2^31 - 1) as the
+// double-precision path, R = sqrt(-2 ln u1) and (cos, sin)(2 pi u2) from the hardware transcendentals
+// (v_log_f32 = log2, v_sqrt_f32, v_sin_f32 / v_cos_f32, whose argument is in revolutions: exactly
+// 2 pi u2), and the noisy coordinate x + scaling * R * {cos, sin} rounded in fp32. Near u1 = 1, where
+// -2 ln u1 is tiny and the fp32 rounding of u1 would dominate it, the series -2 ln(1 - v) =
+// 2 (v + v^2/2 + v^3/3 + v^4/4) of v = (M - k1) / M is used instead (exact integer M - k1 < 2^24,
+// truncation < 2^-30 relative). Not bit-exact with the double path (or glibc): the frames differ in
+// the last fp32 places, so only the statistics can agree -- tools/chanmath_f32_check.hip bounds the
+// errors over every k1 and k2, tests/test_gpu_ber.py checks the published curves in this mode.
+__device__ __forceinline__ float neg2_log_f32(uint32_t k) {   // k in [1, 2^31 - 1]
+  const uint32_t w = 2147483647u - k;
+  const float v = (float)w * (1.0f / 2147483647.0f);
+  const float series = 2.0f * v * (1.0f + v * (0.5f + v * (1.0f / 3.0f + v * 0.25f)));
+  const float u = (float)k * (1.0f / 2147483647.0f);
+  const float lg = -1.38629436111989061883f * __builtin_amdgcn_logf(u);   // -2 ln 2 * log2(u)
+  return w < (1u << 24) ? series : lg;
+}
+__device__ __forceinline__ void box_muller_f32(uint32_t k1, uint32_t k2, float& c, float& s, float& r) {
+  r = __builtin_sqrtf(neg2_log_f32(k1));
+  const float u2 = (float)k2 * (1.0f / 2147483647.0f);
+  c = __builtin_amdgcn_cosf(u2);
+  s = __builtin_amdgcn_sinf(u2);
+}
 
 // Philox4x32-10 with one counter stream per block (key = seed, counter = (block, draw, 0, tag)).
 struct Philox {
@@ -224,12 +249,13 @@ struct ChannelSource {
   float scaling;
   int32_t p_ppm;
   bool hard_demap;
+  bool noise_f32;
   void* out;       // export row of this block, or null
 
   // Draw the info bytes (first in the stream), write them to info_out, prime the encoder.
   __device__ __forceinline__ void init(const ChanArgs& a, int block, bool owner) {
     T = a.r.T; blen = a.r.blen;
-    scaling = a.scaling; p_ppm = a.p_ppm; hard_demap = a.hard_demap != 0;
+    scaling = a.scaling; p_ppm = a.p_ppm; hard_demap = a.hard_demap != 0; noise_f32 = a.noise_f32 != 0;
     rng.init(a.seed, a.first_block + (uint64_t)block);
     const int IB = (blen + 7) >> 3;
 #pragma unroll
@@ -295,18 +321,26 @@ struct ChannelSource {
           y = sym == (uint32_t)k ? pts[2 * k + 1] : y;
         }
       }
-      double u1, u2;
+      uint32_t k1, k2;
       do {
-        u1 = div_rand_max(rng.next());
-        u2 = div_rand_max(rng.next());
-      } while (u1 == 0.0);
-      // R = sqrt(-2 ln u1), (sin, cos)(2 pi u2): channel_math.hpp (a few ulp in double; 2e-8 or fewer
-      // of the fp32 samples differ from glibc's, 268 M host draws, profiles/r04_chanmath_check.txt)
-      const double R = chanmath::sqrt_nonneg(chanmath::neg2_log(u1));
-      double sn, cs;
-      chanmath::sincos_2pi(u2, &sn, &cs);
-      x = (float)((double)x + (double)scaling * (R * cs));
-      y = (float)((double)y + (double)scaling * (R * sn));
+        k1 = rng.next();
+        k2 = rng.next();
+      } while (k1 == 0u);   // u1 == 0 redrawn (gaussian.c:23-27)
+      if (noise_f32) {
+        float cf, sf, rf;
+        box_muller_f32(k1, k2, cf, sf, rf);
+        x = x + scaling * (rf * cf);
+        y = y + scaling * (rf * sf);
+      } else {
+        const double u1 = div_rand_max(k1), u2 = div_rand_max(k2);
+        // R = sqrt(-2 ln u1), (sin, cos)(2 pi u2): channel_math.hpp (a few ulp in double; 2e-8 or
+        // fewer of the fp32 samples differ from glibc's, 268 M host draws, profiles/r04_chanmath_check.txt)
+        const double R = chanmath::sqrt_nonneg(chanmath::neg2_log(u1));
+        double sn, cs;
+        chanmath::sincos_2pi(u2, &sn, &cs);
+        x = (float)((double)x + (double)scaling * (R * cs));
+        y = (float)((double)y + (double)scaling * (R * sn));
+      }
       if (hard_demap) {   // common/hard-demapper.c:66-80: snap to the first nearest point
         float min_val = __builtin_inff();
         float sx = pts[0], sy = pts[1];

@@ -964,6 +964,7 @@ static int simulate_frames_only(ccv_plan* p, uint64_t seed, uint64_t first_block
   if (!hard && !(channel_param >= 0.0 && channel_param < 268435456.0))
     return fail("AWGN noise scaling must be in [0, 2^28)");
   if (hard && (channel_flags & CCV_CHANNEL_HARD_DEMAP)) return fail("the hard demapper belongs to the AWGN channel");
+  if (hard && (channel_flags & CCV_CHANNEL_NOISE_F32)) return fail("the fp32 Box-Muller belongs to the AWGN channel");
   if (nblocks == 0) return 0;
   if (nblocks > 0x7fffffffULL) return fail("too many blocks in one call");
   hipStream_t stream = reinterpret_cast<hipStream_t>(stream_v);
@@ -980,6 +981,7 @@ static int simulate_frames_only(ccv_plan* p, uint64_t seed, uint64_t first_block
   a.scaling = (float)channel_param;
   a.p_ppm = hard ? (int32_t)channel_param : 0;
   a.hard_demap = (channel_flags & CCV_CHANNEL_HARD_DEMAP) != 0;
+  a.noise_f32 = (channel_flags & CCV_CHANNEL_NOISE_F32) != 0;
   a.info_out = d_info;
   a.ch_out = d_channel;
   HIP_TRY(ccv::launch_channel_frames_any(a, p->d.n, p->d.K, p->polys, p->d.gen_mode, hard, stream));
@@ -1040,7 +1042,9 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   a.scaling = (float)channel_param;
   a.p_ppm = hard ? (int32_t)channel_param : 0;
   a.hard_demap = (channel_flags & CCV_CHANNEL_HARD_DEMAP) != 0;
+  a.noise_f32 = (channel_flags & CCV_CHANNEL_NOISE_F32) != 0;
   if (hard && a.hard_demap) return fail("the hard demapper belongs to the AWGN channel");
+  if (hard && a.noise_f32) return fail("the fp32 Box-Muller belongs to the AWGN channel");
   a.info_out = d_info;
   a.ch_out = d_channel;
   // Decisions in LDS (viterbi_channel_lds) for BSC, in HBM scratch for AWGN: the 20 KiB column per

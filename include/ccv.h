@@ -133,6 +133,10 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
  * d_path_metric and d_errors are ignored. The frames are block-major ([nb][T][2^n] / [nb][T]): a
  * CCV_FLAG_STEP_MAJOR plan is rejected (-1). The device sweeps of the sequential decoders use it. */
 #define CCV_CHANNEL_FRAMES_ONLY 2u
+/* AWGN, opt-in: the Box-Muller in fp32 from the hardware log2 / sqrt / sin / cos (same uniforms and
+ * draw order) instead of double precision. Faster; the samples are NOT bit-identical to the double
+ * path or glibc (a few fp32 ulp, tools/chanmath_f32_check.hip), so only the BER statistics match. */
+#define CCV_CHANNEL_NOISE_F32 4u
 int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,
                         int32_t* d_path_metric, unsigned long long* d_errors, void* d_channel,
