@@ -74,7 +74,7 @@ def _check(curve, k, errors, bits, blen):
     return abs(p - p_r) <= tol, f"{curve['name']} point {k}: {p:.4g} ({errors}/{bits}) vs {p_r:.4g} +- {tol:.3g}"
 
 
-def _run(curve, ks, bits_of, decoder):
+def _run(curve, ks, bits_of, decoder, noise="f64"):
     code = CODEBOOK[curve["codebook_index"]]
     soft = curve["channel"] == "awgn"
     pts = [PUB["awgn_ebn0_db"][k] if soft else round(PUB["bsc_p"][k] * 1e6) for k in ks]
@@ -82,7 +82,7 @@ def _run(curve, ks, bits_of, decoder):
     for k, pt in zip(ks, pts):
         (r,) = sim.ber_sweep(code, [pt], SOFT if soft else HARD, bits_per_point=lambda _p: bits_of(k),
                              seed=0xBE4 + k, device_channel=True, hard_demap=curve["hard_demap"],
-                             decoder=decoder, point_index=k)
+                             decoder=decoder, point_index=k, noise_f32=noise == "f32")
         ok, msg = _check(curve, k, r.errors, r.bits, code.blen)
         out.append(msg)
         if not ok:
@@ -94,12 +94,18 @@ def _run(curve, ks, bits_of, decoder):
 VITERBI_AWGN = [c["name"] for c in PUB["curves"] if c["channel"] == "awgn" and c["decoder"] == "viterbi"]
 
 
+# The AWGN curves run twice: with the default double-precision Box-Muller (the reference's arithmetic)
+# and with the opt-in fp32 one (CCV_CHANNEL_NOISE_F32; error bound: tools/chanmath_f32_check.hip).
+NOISE = ["f64", "f32"]
+
+
+@pytest.mark.parametrize("noise", NOISE)
 @pytest.mark.parametrize("name", VITERBI_AWGN)
-def test_viterbi_awgn_curve(torch_cuda, name):
+def test_viterbi_awgn_curve(torch_cuda, name, noise):
     """results/awgn_channel.m:15-28: every soft (code x) and hard-demapper (code xh) Viterbi curve,
     0-14 dB, four times the reference's bits per point (at least 8 M)."""
     curve = _curve(name, "awgn")
-    _run(curve, range(8), lambda k: max(8_000_000, 4 * _ref_bits(curve, k)), "viterbi")
+    _run(curve, range(8), lambda k: max(8_000_000, 4 * _ref_bits(curve, k)), "viterbi", noise)
 
 
 # results/binary_symmetric_channel.m:7 (code 1) disagrees with the reference's own sources: the
@@ -145,13 +151,14 @@ SEQ_AWGN = [c["name"] for c in PUB["curves"] if c["channel"] == "awgn" and c["de
             and c["codebook_index"] != 4]
 
 
+@pytest.mark.parametrize("noise", NOISE)
 @pytest.mark.parametrize("name", SEQ_AWGN)
-def test_sequential_awgn_curve(torch_cuda, name):
+def test_sequential_awgn_curve(torch_cuda, name, noise):
     """results/awgn_channel.m:30-78: stack and Fano curves (soft and hard demapper) of codes
     0/1/2/3/5, 0-10 dB at the reference's bits per point: the on-device channel writes its frames
     to HBM and the sequential decoder reads them."""
     curve = _curve(name, "awgn")
-    _run(curve, range(6), lambda k: _ref_bits(curve, k), curve["decoder"])
+    _run(curve, range(6), lambda k: _ref_bits(curve, k), curve["decoder"], noise)
 
 
 SEQ_BSC = [c["name"] for c in PUB["curves"] if c["channel"] == "bsc" and c["decoder"] != "viterbi"

@@ -783,7 +783,7 @@ def test_streaming_shim_latency_config1(tmp_path):
 
 # --------------------------------------------------------------- on-device channel (ccv_simulate_device)
 
-def _simulate(torch, plan, c, seed, first, nb, param, hard_demap=False):
+def _simulate(torch, plan, c, seed, first, nb, param, hard_demap=False, noise_f32=False):
     hard = plan.channel == HARD
     d_info = torch.empty((nb, c.info_bytes), dtype=torch.uint8, device="cuda")
     d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
@@ -792,7 +792,8 @@ def _simulate(torch, plan, c, seed, first, nb, param, hard_demap=False):
     shape = (nb, c.steps) if hard else (nb, c.steps, 1 << c.n)
     d_ch = torch.empty(shape, dtype=torch.uint8 if hard else torch.float32, device="cuda")
     plan.simulate_device(seed, first, nb, param, d_errors=d_err, d_info=d_info, d_out=d_out,
-                         d_path_metric=d_pm if hard else None, d_channel=d_ch, hard_demap=hard_demap)
+                         d_path_metric=d_pm if hard else None, d_channel=d_ch, hard_demap=hard_demap,
+                         noise_f32=noise_f32)
     torch.cuda.synchronize()
     return (d_info.cpu().numpy(), d_ch.cpu().numpy(), d_out.cpu().numpy(), d_pm.cpu().numpy(),
             int(d_err.item()))
@@ -863,6 +864,60 @@ def test_device_channel_awgn_hard_demapper(torch_cuda, name, c):
     _assert_samples_match(rx, h_rx, hard_demap=True)
     assert np.array_equal(out, O.viterbi_soft(_ocode(c), rx))
     assert err == ch.count_bit_errors(c, info, out)
+
+
+# The opt-in fp32 Box-Muller (CCV_CHANNEL_NOISE_F32) draws the same uniforms as the double-precision
+# path, so its samples track the default's to within the fp32 error of R * (cos, sin): at most
+# F32_NOISE_ABS times the noise scaling over every (k1, k2) (tools/chanmath_f32_check.hip,
+# profiles/r05_noise/chanmath_f32_check.txt), plus the fp32 roundings of the sample and the demapper.
+F32_NOISE_ABS = 4e-6   # measured: 2.38e-6
+F32_CODES = [("k7", K7), ("k9", K9), ("code0", CODEBOOK[0]), ("code5_r13", CODEBOOK[5]),
+             ("k9_true", K9.with_(gen_mode=GEN_TRUE_PARITY))]
+
+
+@pytest.mark.parametrize("hard_demap", [False, True], ids=["demap", "hard_demap"])
+@pytest.mark.parametrize("name,c", F32_CODES, ids=[x[0] for x in F32_CODES])
+def test_device_channel_awgn_f32_noise(torch_cuda, name, c, hard_demap):
+    """CCV_CHANNEL_NOISE_F32: info bits identical to the double-precision channel's; soft decoder
+    input within the fp32 error bound of it (hard-demapped input: equal except for samples within
+    that bound of a decision boundary); the decode of the fp32 samples bit-exact against the oracle;
+    error counts within a handful of the default's."""
+    nb, first = 400, 31337
+    scaling = ch.noise_scaling(2.0)
+    f64 = _simulate(torch_cuda, Plan(c, SOFT), c, 13, first, nb, scaling, hard_demap=hard_demap)
+    f32 = _simulate(torch_cuda, Plan(c, SOFT), c, 13, first, nb, scaling, hard_demap=hard_demap, noise_f32=True)
+    assert np.array_equal(f32[0], f64[0])
+    rx, rx64 = f32[1], f64[1]
+    if hard_demap:
+        diff = int(np.count_nonzero(np.any(rx != rx64, axis=2)))
+        assert diff <= max(4, rx.shape[0] * rx.shape[1] // 10000), diff
+    else:
+        # demapper.c: squared distance / ndist; a sample error e moves it by <= 2 |x - a| e / ndist + e^2
+        eps = 2 * F32_NOISE_ABS * scaling + 2 ** -22 * (1 + 8 * scaling)
+        assert np.max(np.abs(rx - rx64)) <= 8 * eps * (1 + np.max(np.abs(rx64))), np.max(np.abs(rx - rx64))
+    assert np.array_equal(f32[2], O.viterbi_soft(_ocode(c), rx))
+    assert f32[4] == ch.count_bit_errors(c, f32[0], f32[2])
+    assert abs(f32[4] - f64[4]) <= max(8, f64[4] // 100), (f32[4], f64[4])
+
+
+def test_device_channel_f32_noise_frames_only_and_rejections(torch_cuda):
+    """The fp32 noise in the frames-only producer (stack / Fano sweeps) tracks the default the same
+    way; a BSC plan refuses the flag."""
+    from ccviterbi import K15, StackPlan
+    c, nb, s = K15, 200, ch.noise_scaling(3.0)
+    plan = StackPlan(c, SOFT)
+    rxs = []
+    for f32 in (False, True):
+        d_ch = torch_cuda.empty((nb, c.steps, 1 << c.n), dtype=torch_cuda.float32, device="cuda")
+        plan.simulate_frames(5, 77, nb, s, d_ch, noise_f32=f32)
+        torch_cuda.cuda.synchronize()
+        rxs.append(d_ch.cpu().numpy())
+    eps = 2 * F32_NOISE_ABS * s + 2 ** -22 * (1 + 8 * s)
+    assert np.max(np.abs(rxs[1] - rxs[0])) <= 8 * eps * (1 + np.max(np.abs(rxs[0])))
+    plan.close()
+    d_ch = torch_cuda.empty((4, K7.steps), dtype=torch_cuda.uint8, device="cuda")
+    with pytest.raises(Exception, match="AWGN"):
+        Plan(K7, HARD).simulate_frames(1, 0, 4, 50000, d_ch, noise_f32=True)
 
 
 def test_device_channel_ber_sweep_matches_host(torch_cuda):

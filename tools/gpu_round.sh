@@ -5,6 +5,9 @@
 #   bench     the bench line of every BASELINE config (+ the textbook codes, Fano), CPU baselines
 #   prof      rocprofv3 kernel stats of the headline bench
 #   sweeps    Eb/N0 sweeps of configs 2 and 3 with the on-device channel (800 M bits per point)
+#   noise     the same sweeps (k9, k7, seed-paired) with the opt-in fp32 Box-Muller against the default
+#             double one (tools/noise_compare.py), and the exhaustive fp32 error check
+#             (tools/chanmath_f32_check, built on the CPU side beforehand)
 #   refdriver the unchanged reference AWGN driver (AWGN-channel/main.c) over libccv_awgn.so, code 0,
 #             all eight points, checked against the published table (~7 minutes)
 # Each GPU step has its own time limit; a crash / timeout ends the session (test FAILURES do not).
@@ -58,6 +61,21 @@ if has sweeps; then
 import json, sys
 for l in sys.stdin:
     d = json.loads(l); print('$c', d['ebn0_db'], d['errors'], d['bits'], d['mbit_s'])"
+  done
+fi
+if has noise; then
+  if [ -x tools/chanmath_f32_check ]; then
+    timeout -k 10 120 tools/chanmath_f32_check > $OUT/chanmath_f32_check.txt 2>&1 \
+        || { echo "chanmath_f32_check failed"; tail -5 $OUT/chanmath_f32_check.txt; exit 1; }
+    cat $OUT/chanmath_f32_check.txt
+  fi
+  for c in k9 k7 k9:true k7:true; do
+    tag=$(echo $c | tr -d ':')
+    for nz in f64 f32; do
+      timeout -k 10 300 python -m ccviterbi.sim --code $c --points 10:14 --device-channel --noise $nz \
+          > $OUT/noise_${tag}_$nz.log 2>&1 || { echo "sweep $c $nz failed"; tail -3 $OUT/noise_${tag}_$nz.log; exit 1; }
+    done
+    python tools/noise_compare.py $OUT/noise_${tag}_f64.log $OUT/noise_${tag}_f32.log $OUT/noise_${tag}.json
   done
 fi
 if has refdriver; then
