@@ -70,8 +70,11 @@ __device__ __forceinline__ float neg2_log_f32(uint32_t k) {   // k in [1, 2^31 -
   const float lg = -1.38629436111989061883f * __builtin_amdgcn_logf(u);   // -2 ln 2 * log2(u)
   return w < (1u << 24) ? series : lg;
 }
+// R = sqrt(-2 ln u1) with the raw v_sqrt_f32 (1 ulp; its argument is >= 9.3e-10, never denormal, so
+// the IEEE sqrt's scaling and two correction steps buy nothing here)
+__device__ __forceinline__ float radius_f32(uint32_t k1) { return __builtin_amdgcn_sqrtf(neg2_log_f32(k1)); }
 __device__ __forceinline__ void box_muller_f32(uint32_t k1, uint32_t k2, float& c, float& s, float& r) {
-  r = __builtin_sqrtf(neg2_log_f32(k1));
+  r = radius_f32(k1);
   const float u2 = (float)k2 * (1.0f / 2147483647.0f);
   c = __builtin_amdgcn_cosf(u2);
   s = __builtin_amdgcn_sinf(u2);
@@ -110,6 +113,20 @@ struct Philox {
     b0 = b1; b1 = b2; b2 = b3;
     ++used;
     return r >> 1;
+  }
+  // the next two values (x first): one refill site and selects instead of two next() (a pair
+  // straddles a refill when one word is left, used == 3)
+  __device__ __forceinline__ void next2(uint32_t& x, uint32_t& y) {
+    const bool odd = used == 3;
+    const uint32_t last = b0;
+    if (used >= 3) refill();
+    x = (odd ? last : b0) >> 1;
+    y = (odd ? b0 : b1) >> 1;
+    const uint32_t n0 = odd ? b1 : b2, n1 = odd ? b2 : b3;
+    b2 = b3;   // meaningful only when odd (three words left)
+    b0 = n0;
+    b1 = n1;
+    used = odd ? 1 : used + 2;
   }
 };
 
@@ -157,49 +174,71 @@ struct Constellation<3> {
                                     -0.408248f, -0.408248f, -0.408248f, -1.224745f};
 };
 
-// Encoder (common/encoder.c:84-119) one step at a time; the info bits sit in a window of up to 8
-// 32-bit words consumed MSB-first, shifted by whole words so every index is static.
+// Encoder (common/encoder.c:84-119), bit-sliced over 32 steps: output stream k of step t is the parity
+// of the taps j of poly k over the info bits i(t - j) (the reference's shift register holds i(t - j)
+// at bit 63 - j), so a whole word of it is the XOR of the info word shifted right by each tap j
+// (funnelled with the previous word), computed once per 32 steps; the x86 idiom (GEN_REF_X86: the
+// result cleared when the taps at register bits 4 mod 8 have odd parity) is one more such XOR. Per
+// step: the symbol's bits are the streams' top bits, then one shift each. The info window w[0..7]
+// holds the bits MSB-first, cleared from blen on (the tail steps shift in zeros).
 template <CodeSpec C>
 struct Encoder {
+  static_assert(C.K >= 2 && C.K <= 32, "bit-sliced encoder: taps within one word");
   uint32_t w[8];
-  uint32_t state;
+  uint32_t e[C.n];   // stream k of the current 32-step word, the current step in bit 31
   int t;
-  __device__ __forceinline__ uint32_t symbol_and_advance(int blen) {
-    const uint32_t i = bit(blen);
-    const uint64_t sr = ((uint64_t)state << (64 - C.K)) | ((uint64_t)i << 63);
-    uint32_t e = 0;
+  __device__ __forceinline__ void start(int blen) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int valid = blen - 32 * k;
+      w[k] &= valid >= 32 ? ~0u : (valid <= 0 ? 0u : ~0u << (32 - valid));
+    }
+    t = 0;
+    fill(0u, w[0]);
+  }
+  __device__ __forceinline__ void fill(uint32_t prev, uint32_t cur) {
 #pragma unroll
     for (int k = 0; k < C.n; ++k) {
-      const uint64_t v = sr & C.poly[k];
-      uint32_t p = (uint32_t)__popcll(v) & 1u;
-      if (C.gen == GEN_REF_X86) p &= ((uint32_t)__popcll(v & 0x1010101010101010ull) & 1u) ^ 1u;
-      e = (e << 1) | p;
+      uint32_t x = 0, tw = 0;
+#pragma unroll
+      for (int j = 0; j < C.K; ++j) {
+        if (((C.poly[k] >> (63 - j)) & 1u) == 0) continue;
+        uint32_t s = cur;
+        if (j > 0) s = (cur >> j) | (prev << (32 - j));
+        x ^= s;
+        if (C.gen == GEN_REF_X86 && (63 - j) % 8 == 4) tw ^= s;
+      }
+      e[k] = C.gen == GEN_REF_X86 ? (x & ~tw) : x;
     }
-    state = (state >> 1) | (i << (C.K - 2));
-    advance(blen);
-    return e;
   }
-  // the next info bit (0 past blen) is the top bit of w[0]; the window moves by a word every 32
-  // steps behind a real (wave-uniform) branch: the empty volatile asm keeps the compiler from
-  // speculating the word shift into 7 selects on every step
-  __device__ __forceinline__ uint32_t bit(int blen) const { return t < blen ? (w[0] >> 31) : 0u; }
-  __device__ __forceinline__ void advance(int) {
+  // bit 31 = output bit k of the current step (k = 0: the symbol's MSB)
+  __device__ __forceinline__ uint32_t msb(int k) const { return e[k] & 0x80000000u; }
+  __device__ __forceinline__ uint32_t symbol() const {
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < C.n; ++k) s = (s << 1) | (e[k] >> 31);
+    return s;
+  }
+  // the window moves by a word every 32 steps behind a real (wave-uniform) branch: the empty volatile
+  // asm keeps the compiler from speculating the word shift into selects on every step
+  __device__ __forceinline__ void advance() {
     ++t;
     if ((t & 31) == 0) {
+      const uint32_t prev = w[0];
 #pragma unroll
       for (int k = 0; k < 7; ++k) w[k] = w[k + 1];
       w[7] = 0;
+      fill(prev, w[0]);
       asm volatile("");
     } else {
-      w[0] <<= 1;
+#pragma unroll
+      for (int k = 0; k < C.n; ++k) e[k] <<= 1;
     }
   }
 };
 
-// Per-lane source of one block's decoder input, in decoder order. HARD: BM = Hamming distances of
-// the received symbol; soft: BM = demapped squared distances.
 // Encoder of a code known only at run time (ccv_simulate_device CCV_CHANNEL_FRAMES_ONLY: any plan, K <=
-// 64): the same register window and shift-register arithmetic as Encoder<C>, with a 64-bit state.
+// 64): the reference's shift-register arithmetic step by step, with a 64-bit state; the same window.
 template <int NP>
 struct EncoderRT {
   uint32_t w[8];
@@ -207,8 +246,17 @@ struct EncoderRT {
   int t;
   int K, gen;
   uint64_t poly[NP];
-  __device__ __forceinline__ uint32_t symbol_and_advance(int blen) {
-    const uint64_t i = bit(blen);
+  __device__ __forceinline__ void start(int blen) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int valid = blen - 32 * k;
+      w[k] &= valid >= 32 ? ~0u : (valid <= 0 ? 0u : ~0u << (32 - valid));
+    }
+    state = 0;
+    t = 0;
+  }
+  __device__ __forceinline__ uint32_t symbol() const {
+    const uint64_t i = w[0] >> 31;
     const uint64_t sr = (K < 64 ? state << (64 - K) : state) | (i << 63);
     uint32_t e = 0;
 #pragma unroll
@@ -218,15 +266,11 @@ struct EncoderRT {
       if (gen == GEN_REF_X86) p &= ((uint32_t)__popcll(v & 0x1010101010101010ull) & 1u) ^ 1u;
       e = (e << 1) | p;
     }
-    state = (state >> 1) | (i << (K - 2));
-    advance(blen);
     return e;
   }
-  // the next info bit (0 past blen) is the top bit of w[0]; the window moves by a word every 32
-  // steps behind a real (wave-uniform) branch: the empty volatile asm keeps the compiler from
-  // speculating the word shift into 7 selects on every step
-  __device__ __forceinline__ uint32_t bit(int blen) const { return t < blen ? (w[0] >> 31) : 0u; }
-  __device__ __forceinline__ void advance(int) {
+  __device__ __forceinline__ uint32_t msb(int k) const { return ((symbol() >> (NP - 1 - k)) & 1u) << 31; }
+  __device__ __forceinline__ void advance() {
+    state = (state >> 1) | ((uint64_t)(w[0] >> 31) << (K - 2));
     ++t;
     if ((t & 31) == 0) {
 #pragma unroll
@@ -286,8 +330,7 @@ struct ChannelSource {
       for (int k = 0; k < 7; ++k) enc.w[k] = (enc.w[k] << sb) | (enc.w[k + 1] >> (32 - sb));
       enc.w[7] <<= sb;
     }
-    enc.state = 0;
-    enc.t = 0;
+    enc.start(blen);
     out = a.ch_out && owner
               ? (void*)((char*)a.ch_out + (size_t)block * T * (HARD ? 1 : NS * sizeof(float)))
               : nullptr;
@@ -295,11 +338,18 @@ struct ChannelSource {
 
   __device__ __forceinline__ void next(MT (&BM)[NS]) {
     const int t = enc.t;
-    uint32_t sym = enc.symbol_and_advance(blen);
     if constexpr (HARD) {
+      uint32_t sym = enc.symbol();
+      enc.advance();
+      if constexpr (C.n == 2) {   // draw k flips bit k
+        uint32_t r0, r1;
+        rng.next2(r0, r1);
+        sym ^= ((int32_t)(r0 % 1000000u) < p_ppm ? 1u : 0u) | ((int32_t)(r1 % 1000000u) < p_ppm ? 2u : 0u);
+      } else {
 #pragma unroll
-      for (int k = 0; k < C.n; ++k)
-        if ((int32_t)(rng.next() % 1000000u) < p_ppm) sym ^= 1u << k;
+        for (int k = 0; k < C.n; ++k)
+          if ((int32_t)(rng.next() % 1000000u) < p_ppm) sym ^= 1u << k;
+      }
 #pragma unroll
       for (int k = 0; k < NS; ++k) BM[k] = (uint32_t)__builtin_popcount((uint32_t)k ^ sym);
       if (out && t < T) reinterpret_cast<uint8_t*>(out)[t] = (uint8_t)sym;
@@ -312,20 +362,24 @@ struct ChannelSource {
         // y <- bit 0; n = 1: both <- bit 0) -- two sign flips instead of a compare-select chain
         static_assert(pts[0] == pts[1] && (C.n == 1 ? pts[2] == -pts[0] : pts[4] == -pts[0] && pts[3] == -pts[1]));
         const uint32_t a = __builtin_bit_cast(uint32_t, pts[0]);
-        x = __builtin_bit_cast(float, a ^ (((sym >> (C.n - 1)) & 1u) << 31));
-        y = __builtin_bit_cast(float, a ^ ((sym & 1u) << 31));
+        x = __builtin_bit_cast(float, a ^ enc.msb(0));
+        y = __builtin_bit_cast(float, a ^ enc.msb(C.n - 1));
       } else {
+        const uint32_t sym = enc.symbol();
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
           x = sym == (uint32_t)k ? pts[2 * k] : x;
           y = sym == (uint32_t)k ? pts[2 * k + 1] : y;
         }
       }
+      enc.advance();
       uint32_t k1, k2;
-      do {
-        k1 = rng.next();
-        k2 = rng.next();
-      } while (k1 == 0u);   // u1 == 0 redrawn (gaussian.c:23-27)
+      rng.next2(k1, k2);
+      if (__builtin_expect(k1 == 0u, 0)) {   // u1 == 0 redrawn (gaussian.c:23-27)
+        do {
+          rng.next2(k1, k2);
+        } while (k1 == 0u);
+      }
       if (noise_f32) {
         float cf, sf, rf;
         box_muller_f32(k1, k2, cf, sf, rf);

@@ -29,7 +29,7 @@ __global__ void check_r(float* abs_err, float* rel_err, float* rmax) {
        k += (uint64_t)gridDim.x * blockDim.x) {
     const double u1 = ccv::div_rand_max((uint32_t)k);
     const double r64 = ccv::chanmath::sqrt_nonneg(ccv::chanmath::neg2_log(u1));
-    const float r32 = __builtin_sqrtf(ccv::neg2_log_f32((uint32_t)k));
+    const float r32 = ccv::radius_f32((uint32_t)k);
     const double e = fabs((double)r32 - r64);
     int bin = (int)floor(-log10(u1));
     bin = bin < 0 ? 0 : (bin >= kBins ? kBins - 1 : bin);
