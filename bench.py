@@ -267,14 +267,23 @@ PMC_SCALE_NOTE = ("FETCH_SIZE x 2, WRITE_SIZE x 1 as the guide prescribes for gf
                   "(hbm_read_gbs), which is impossible; x 2 is the consistent reading.")
 
 
+HBM_PROBE_MIN_BYTES = 104 * 25000 * 46 * 16   # the headline's input batch, 1.91 GB
+LATENCY_BOUND_BELOW = 0.35   # roofline.bound "latency" when both measured fractions are below this
+
+
 def measure_hbm_ceiling(d_buf, stream, reps=5):
     """Achievable HBM rates on this box: ccv_hbm_probe's streaming copy of d_buf (read + write bytes)
     and its read-only stream of d_buf, each the best of `reps` HIP-event-timed launches on `stream`
-    after one untimed launch. GB/s."""
+    after one untimed launch. GB/s. A batch smaller than the headline's (hard input, few frames) is
+    replaced by a random buffer of the headline's 1.91 GB: on a small buffer the launch overhead and
+    ramp, not the HBM, set the rate (a 18 MB batch streams at ~4.3 TB/s)."""
     import torch
     from ccviterbi import _native
     L = _native.core()
     nbytes = d_buf.numel() * d_buf.element_size() // 16 * 16
+    if nbytes < HBM_PROBE_MIN_BYTES:
+        d_buf = torch.randint(0, 256, (HBM_PROBE_MIN_BYTES,), dtype=torch.uint8, device=d_buf.device)
+        nbytes = HBM_PROBE_MIN_BYTES
     dst = torch.empty(nbytes, dtype=torch.uint8, device=d_buf.device)
     sink = torch.zeros(1, dtype=torch.int32, device=d_buf.device)
     out = {}
@@ -308,7 +317,7 @@ def hbm_ceiling_fields(probe, traffic, kernel_ms):
     return {"hbm_copy_gbs": round(probe["copy"], 1), "hbm_read_gbs": round(probe["read"], 1),
             "achievable_gbs": round(ach, 1),
             "achievable_basis": "max of ccv_hbm_probe copy (read+write bytes) and read-only stream over "
-                                "the input batch, best of 5, this run",
+                                "the input batch (at least 1.91 GB), best of 5, this run",
             "traffic_frac_of_achievable": (round(traffic / (kernel_ms * 1e-3) / 1e9 / ach, 4)
                                            if traffic else None)}
 
@@ -541,6 +550,16 @@ def main(argv=None):
             bound_basis = ("the larger of traffic_frac (PMC HBM bytes / kernel time / 8 TB/s) and "
                            "valu_frac (SQ_INSTS_VALU / (512 per cycle x GRBM_GUI_ACTIVE / 8)); "
                            "frac / achieved / peak stay the SURVEY 8(d) HBM figure")
+            if max(valu_frac, traffic_frac) < LATENCY_BOUND_BELOW:
+                # neither pipe is near busy: the waves' dependent chains (and, for the sequential
+                # decoders, lanes idle behind the longest searches) set the time
+                stall = pmc.get("stall") or {}
+                bound = "latency"
+                bound_basis = (f"traffic_frac {traffic_frac:.3f} and valu_frac {valu_frac:.3f} both below "
+                               f"{LATENCY_BOUND_BELOW}: neither HBM nor VALU issue binds; waves waiting "
+                               f"{stall.get('sq_wait_any_frac', float('nan')):.2f} / issue-stalled "
+                               f"{stall.get('sq_wait_inst_any_frac', float('nan')):.2f} of their lifetime "
+                               "(PMC stall pass)")
         else:
             bound = None   # not derived: no committed PMC pass for this workload
             bound_basis = (f"unmeasured: no PMC pass committed for workload key {workload_key!r} "

@@ -140,16 +140,18 @@ class DeviceChannelDecoder:
     def warm_up(self, seconds: float, point: Optional[float] = None) -> int:
         """Decode throw-away slices (blocks 2^62.., a Philox range no point uses) until `seconds` have
         passed: the GPU's clock ramp (~35 ms of load) and the first launches then stay
-        out of the first point's time. A slice is a few frames (one frame for the stack / Fano
-        decoders), so the limit is kept to within one slice. The Viterbi kernels run at `point` (the
-        sweep's first point; their time does not depend on the noise); the sequential decoders at a
-        low-noise point (10 dB / 1,000 ppm), where no search runs into its timeout. Returns the
+        out of the first point's time. A Viterbi slice is one whole chunk (the launch size of the
+        points: small launches leave the chip below the power state the points run at, and the first
+        points of a sweep came out 10-25 % slow); the stack / Fano decoders run one
+        frame per slice, so the limit is kept to within one slice. The Viterbi kernels run at `point`
+        (the sweep's first point; their time does not depend on the noise); the sequential decoders
+        at a low-noise point (10 dB / 1,000 ppm), where no search runs into its timeout. Returns the
         slices run."""
         import time
         seq = self.seq is not None
         if seq or point is None:
             point = (10.0 if seq else 4.0) if self.channel == SOFT else (1000 if seq else 50000)
-        nb = min(self.chunk, self.frame_blocks * (1 if seq else 4))
+        nb = min(self.chunk, self.frame_blocks) if seq else self.chunk
         n, t0 = 0, time.perf_counter()
         while n == 0 or time.perf_counter() - t0 < seconds:
             self(point, 1 << 62, nb)
