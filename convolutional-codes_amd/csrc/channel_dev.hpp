@@ -428,6 +428,23 @@ struct ChannelSource {
   }
 };
 
+// step(t) for t in [t0, t1), unrolled by U = K - 1 with a rolled remainder. An in-place trellis step
+// leaves new state j in the register old state 2j held (acs_step), a permutation of period K - 1: a
+// rolled loop pays ~30 register copies per step at its back edge to put every metric back, an
+// unrolled period none.
+template <int U, class F>
+__device__ __forceinline__ void for_steps(int t0, int t1, F&& step) {
+  int t = t0;
+#pragma unroll 1
+  for (; t + U <= t1; t += U) {
+    [&]<int... u>(std::integer_sequence<int, u...>) __attribute__((always_inline)) {
+      (step(t + u), ...);
+    }(std::make_integer_sequence<int, U>{});
+  }
+#pragma unroll 1
+  for (; t < t1; ++t) step(t);
+}
+
 // K <= 7: one lane per block (acs_reg.hpp), input generated in registers.
 template <CodeSpec C, bool HARD>
 __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
@@ -450,12 +467,11 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
     else M[s] = s ? __builtin_inff() : 0.0f;
   }
   auto run = [&](auto sat, int t0, int t1) {
-#pragma unroll 1
-    for (int t = t0; t < t1; ++t) {
+    for_steps<C.K - 1>(t0, t1, [&](int t) __attribute__((always_inline)) {
       MT BM[NS];
       src.next(BM);
       dec[(size_t)t * dstride] = acs_step<C, decltype(sat)::value, MT>(M, BM);
-    }
+    });
   };
   // BSC saturation (reference :127-130) only matters while states are unreachable (t < K-1);
   // afterwards the hard ACS runs on 16-bit metrics (uint16_t), like viterbi_hard_reg
@@ -465,8 +481,7 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
     uint16_t M16[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) M16[s] = (uint16_t)M[s];
-#pragma unroll 1
-    for (int t = t0; t < T; ++t) {
+    for_steps<C.K - 1>(t0, T, [&](int t) __attribute__((always_inline)) {
       MT BM[NS];
       src.next(BM);
       uint16_t B16[NS];
@@ -476,7 +491,7 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
         asm volatile("" : "+v"(B16[k]));   // no v_bcnt-folded adds
       }
       dec[(size_t)t * dstride] = acs_step<C, false, uint16_t>(M16, B16);
-    }
+    });
 #pragma unroll
     for (int s = 0; s < S; ++s) M[s] = M16[s];
   } else {
@@ -575,12 +590,11 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
       growth_step<C, ts, MT>(M, BM, HARD ? (MT)0xFF00u : (MT)__builtin_inff());
     }(), ...);
   }(std::make_integer_sequence<int, G>{});
-#pragma unroll 1
-  for (int t = G; t < T; ++t) {
+  for_steps<C.K - 1>(G, T, [&](int t) __attribute__((always_inline)) {
     MT BM[NS];
     next_bm(BM);
     dl[(size_t)(t - G) * kRegThreads + lane] = acs_step<C, false, MT>(M, BM);
-  }
+  });
   // each lane reads back only its own column: no barrier
   using AM = typename std::conditional<std::is_same_v<MT, uint16_t>, uint32_t, float>::type;
   AM Ma[S];
