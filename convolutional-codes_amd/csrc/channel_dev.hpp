@@ -283,7 +283,10 @@ struct EncoderRT {
   }
 };
 
-template <CodeSpec C, bool HARD, class Enc = Encoder<C>>
+// F32: the opt-in fp32 Box-Muller (CCV_CHANNEL_NOISE_F32) -- a compile-time choice, so the fp32
+// kernels do not hold the double-precision path's registers (108 instead of 157 VGPRs at K = 7 true
+// parity: one more wave per SIMD).
+template <CodeSpec C, bool HARD, class Enc = Encoder<C>, bool F32 = false>
 struct ChannelSource {
   static constexpr int NS = 1 << C.n;
   using MT = typename std::conditional<HARD, uint32_t, float>::type;
@@ -293,13 +296,12 @@ struct ChannelSource {
   float scaling;
   int32_t p_ppm;
   bool hard_demap;
-  bool noise_f32;
   void* out;       // export row of this block, or null
 
   // Draw the info bytes (first in the stream), write them to info_out, prime the encoder.
   __device__ __forceinline__ void init(const ChanArgs& a, int block, bool owner) {
     T = a.r.T; blen = a.r.blen;
-    scaling = a.scaling; p_ppm = a.p_ppm; hard_demap = a.hard_demap != 0; noise_f32 = a.noise_f32 != 0;
+    scaling = a.scaling; p_ppm = a.p_ppm; hard_demap = a.hard_demap != 0;
     rng.init(a.seed, a.first_block + (uint64_t)block);
     const int IB = (blen + 7) >> 3;
 #pragma unroll
@@ -336,9 +338,104 @@ struct ChannelSource {
               : nullptr;
   }
 
+  // A soft step in two phases: draw() -- the symbol's bits from the encoder and the step's two
+  // uniforms (the branches: Philox refill, window shift, the u1 = 0 redraw) -- then compute() -- the
+  // noise, the demapper, the branch metrics. (Round 5 measured a software-pipelined loop that puts
+  // step t + 1's compute() in one basic block with step t's ACS: hipcc does not interleave them, and
+  // it ran within 1 % of the plain loop, profiles/r05_chan/.)
+  struct Draw {
+    uint32_t sx, sy;   // n <= 2: the sign words of the point's coordinates; n = 3: sx = the symbol
+    uint32_t k1, k2;
+    int t;
+  };
+  __device__ __forceinline__ Draw draw() {
+    Draw d;
+    d.t = enc.t;
+    if constexpr (C.n <= 2) {
+      d.sx = enc.msb(0);
+      d.sy = enc.msb(C.n - 1);
+    } else {
+      d.sx = enc.symbol();
+      d.sy = 0;
+    }
+    enc.advance();
+    rng.next2(d.k1, d.k2);
+    if (__builtin_expect(d.k1 == 0u, 0)) {   // u1 == 0 redrawn (gaussian.c:23-27)
+      do {
+        rng.next2(d.k1, d.k2);
+      } while (d.k1 == 0u);
+    }
+    return d;
+  }
+  __device__ __forceinline__ void compute(const Draw& d, float (&BM)[NS]) const {
+    static_assert(C.n >= 1 && C.n <= 3, "the reference has constellations for n = 1..3");
+    constexpr const float* pts = Constellation<C.n>::pts;
+    float x = 0.f, y = 0.f;
+    if constexpr (C.n <= 2) {
+      // n = 1, 2: the points are (+-a, +-a), the signs the symbol's bits (n = 2: x <- bit 1,
+      // y <- bit 0; n = 1: both <- bit 0) -- two sign flips instead of a compare-select chain
+      static_assert(pts[0] == pts[1] && (C.n == 1 ? pts[2] == -pts[0] : pts[4] == -pts[0] && pts[3] == -pts[1]));
+      const uint32_t a = __builtin_bit_cast(uint32_t, pts[0]);
+      x = __builtin_bit_cast(float, a ^ d.sx);
+      y = __builtin_bit_cast(float, a ^ d.sy);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        x = d.sx == (uint32_t)k ? pts[2 * k] : x;
+        y = d.sx == (uint32_t)k ? pts[2 * k + 1] : y;
+      }
+    }
+    if constexpr (F32) {
+      float cf, sf, rf;
+      box_muller_f32(d.k1, d.k2, cf, sf, rf);
+      x = x + scaling * (rf * cf);
+      y = y + scaling * (rf * sf);
+    } else {
+      const double u1 = div_rand_max(d.k1), u2 = div_rand_max(d.k2);
+      // R = sqrt(-2 ln u1), (sin, cos)(2 pi u2): channel_math.hpp (a few ulp in double; 2e-8 or
+      // fewer of the fp32 samples differ from glibc's, 268 M host draws, profiles/r04_chanmath_check.txt)
+      const double R = chanmath::sqrt_nonneg(chanmath::neg2_log(u1));
+      double sn, cs;
+      chanmath::sincos_2pi(u2, &sn, &cs);
+      x = (float)((double)x + (double)scaling * (R * cs));
+      y = (float)((double)y + (double)scaling * (R * sn));
+    }
+    if (hard_demap) {   // common/hard-demapper.c:66-80: snap to the first nearest point
+      float min_val = __builtin_inff();
+      float sx = pts[0], sy = pts[1];
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const float dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
+        const float dd = (dx * dx) + (dy * dy);
+        const bool lt = dd < min_val;
+        min_val = lt ? dd : min_val;
+        sx = lt ? pts[2 * k] : sx;
+        sy = lt ? pts[2 * k + 1] : sy;
+      }
+      x = sx;
+      y = sy;
+    }
+    constexpr float ndx = pts[0] - pts[2], ndy = pts[1] - pts[3];
+    constexpr float nd = (ndx * ndx) + (ndy * ndy);
+    // the points as compile-time constants (a loop over pts[] reads them from memory), so the
+    // coordinates the points share give one subtraction and one square each
+    [&]<int... k>(std::integer_sequence<int, k...>) __attribute__((always_inline)) {
+      ((BM[k] = div_const<nd>(((x - Constellation<C.n>::pts[2 * k]) * (x - Constellation<C.n>::pts[2 * k])) +
+                              ((y - Constellation<C.n>::pts[2 * k + 1]) * (y - Constellation<C.n>::pts[2 * k + 1])))),
+       ...);
+    }(std::make_integer_sequence<int, NS>{});
+  }
+  __device__ __forceinline__ void export_soft(int t, const float (&BM)[NS]) const {
+    if (out && t < T) {
+      float* o = reinterpret_cast<float*>(out) + (size_t)t * NS;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) o[k] = BM[k];
+    }
+  }
+
   __device__ __forceinline__ void next(MT (&BM)[NS]) {
-    const int t = enc.t;
     if constexpr (HARD) {
+      const int t = enc.t;
       uint32_t sym = enc.symbol();
       enc.advance();
       if constexpr (C.n == 2) {   // draw k flips bit k
@@ -354,76 +451,9 @@ struct ChannelSource {
       for (int k = 0; k < NS; ++k) BM[k] = (uint32_t)__builtin_popcount((uint32_t)k ^ sym);
       if (out && t < T) reinterpret_cast<uint8_t*>(out)[t] = (uint8_t)sym;
     } else {
-      static_assert(C.n >= 1 && C.n <= 3, "the reference has constellations for n = 1..3");
-      constexpr const float* pts = Constellation<C.n>::pts;
-      float x = 0.f, y = 0.f;
-      if constexpr (C.n <= 2) {
-        // n = 1, 2: the points are (+-a, +-a), the signs the symbol's bits (n = 2: x <- bit 1,
-        // y <- bit 0; n = 1: both <- bit 0) -- two sign flips instead of a compare-select chain
-        static_assert(pts[0] == pts[1] && (C.n == 1 ? pts[2] == -pts[0] : pts[4] == -pts[0] && pts[3] == -pts[1]));
-        const uint32_t a = __builtin_bit_cast(uint32_t, pts[0]);
-        x = __builtin_bit_cast(float, a ^ enc.msb(0));
-        y = __builtin_bit_cast(float, a ^ enc.msb(C.n - 1));
-      } else {
-        const uint32_t sym = enc.symbol();
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-          x = sym == (uint32_t)k ? pts[2 * k] : x;
-          y = sym == (uint32_t)k ? pts[2 * k + 1] : y;
-        }
-      }
-      enc.advance();
-      uint32_t k1, k2;
-      rng.next2(k1, k2);
-      if (__builtin_expect(k1 == 0u, 0)) {   // u1 == 0 redrawn (gaussian.c:23-27)
-        do {
-          rng.next2(k1, k2);
-        } while (k1 == 0u);
-      }
-      if (noise_f32) {
-        float cf, sf, rf;
-        box_muller_f32(k1, k2, cf, sf, rf);
-        x = x + scaling * (rf * cf);
-        y = y + scaling * (rf * sf);
-      } else {
-        const double u1 = div_rand_max(k1), u2 = div_rand_max(k2);
-        // R = sqrt(-2 ln u1), (sin, cos)(2 pi u2): channel_math.hpp (a few ulp in double; 2e-8 or
-        // fewer of the fp32 samples differ from glibc's, 268 M host draws, profiles/r04_chanmath_check.txt)
-        const double R = chanmath::sqrt_nonneg(chanmath::neg2_log(u1));
-        double sn, cs;
-        chanmath::sincos_2pi(u2, &sn, &cs);
-        x = (float)((double)x + (double)scaling * (R * cs));
-        y = (float)((double)y + (double)scaling * (R * sn));
-      }
-      if (hard_demap) {   // common/hard-demapper.c:66-80: snap to the first nearest point
-        float min_val = __builtin_inff();
-        float sx = pts[0], sy = pts[1];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-          const float dx = x - pts[2 * k], dy = y - pts[2 * k + 1];
-          const float d = (dx * dx) + (dy * dy);
-          const bool lt = d < min_val;
-          min_val = lt ? d : min_val;
-          sx = lt ? pts[2 * k] : sx;
-          sy = lt ? pts[2 * k + 1] : sy;
-        }
-        x = sx;
-        y = sy;
-      }
-      constexpr float ndx = pts[0] - pts[2], ndy = pts[1] - pts[3];
-      constexpr float nd = (ndx * ndx) + (ndy * ndy);
-      // the points as compile-time constants (a loop over pts[] reads them from memory), so the
-      // coordinates the points share give one subtraction and one square each
-      [&]<int... k>(std::integer_sequence<int, k...>) __attribute__((always_inline)) {
-        ((BM[k] = div_const<nd>(((x - Constellation<C.n>::pts[2 * k]) * (x - Constellation<C.n>::pts[2 * k])) +
-                                ((y - Constellation<C.n>::pts[2 * k + 1]) * (y - Constellation<C.n>::pts[2 * k + 1])))),
-         ...);
-      }(std::make_integer_sequence<int, NS>{});
-      if (out && t < T) {
-        float* o = reinterpret_cast<float*>(out) + (size_t)t * NS;
-#pragma unroll
-        for (int k = 0; k < NS; ++k) o[k] = BM[k];
-      }
+      const Draw d = draw();
+      compute(d, BM);
+      export_soft(d.t, BM);
     }
   }
 };
@@ -446,12 +476,12 @@ __device__ __forceinline__ void for_steps(int t0, int t1, F&& step) {
 }
 
 // K <= 7: one lane per block (acs_reg.hpp), input generated in registers.
-template <CodeSpec C, bool HARD>
+template <CodeSpec C, bool HARD, bool F32 = false>
 __global__ __launch_bounds__(kRegThreads) void viterbi_channel_reg(ChanArgs a) {
   constexpr int S = 1 << (C.K - 1);
   constexpr int NS = 1 << C.n;
   using DW = DecWord<S>;
-  using Src = ChannelSource<C, HARD>;
+  using Src = ChannelSource<C, HARD, Encoder<C>, F32>;
   using MT = typename Src::MT;
   const int b = blockIdx.x * kRegThreads + threadIdx.x;
   const int T = a.r.T, nb = a.r.nblocks;
@@ -547,13 +577,13 @@ __device__ __forceinline__ uint32_t traceback_lds(const RegArgs& a, const DW* co
   return owner ? errors : 0u;
 }
 
-template <CodeSpec C, bool HARD>
+template <CodeSpec C, bool HARD, bool F32 = false>
 __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   constexpr int S = 1 << (C.K - 1);
   constexpr int NS = 1 << C.n;
   constexpr int G = C.K - 1;
   using DW = DecWord<S>;
-  using Src = ChannelSource<C, HARD>;
+  using Src = ChannelSource<C, HARD, Encoder<C>, F32>;
   using SM = typename Src::MT;                                      // source metric type
   // ACS metric type: uint16_t for the BSC (fp32, exact here as in the persistent BSC kernel,
   // acs_persist.hpp, measured 1 % slower in this kernel, whose time is the channel's: 108.7-109.7 vs
@@ -616,10 +646,10 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
 // Rows go out through LDS, 8 steps at a time: lane-per-row 16-byte stores put one wave's 64 stores
 // in 64 different 128-byte lines, which L2 evicts half-written (WRITE_SIZE 2.5x the frame bytes,
 // DESIGN.md 4.4); staged, store instruction j writes rows 8j .. 8j+7, 8 lanes per 128-byte line.
-template <CodeSpec C, bool HARD>
+template <CodeSpec C, bool HARD, bool F32 = false>
 __global__ __launch_bounds__(kRegThreads) void channel_frames(ChanArgs a) {
   static_assert(!HARD && C.n == 2, "soft r = 1/2 frames");
-  using Src = ChannelSource<C, HARD>;
+  using Src = ChannelSource<C, HARD, Encoder<C>, F32>;
   constexpr int CH = 8;   // steps per staged chunk: CH x 16 B = one 128-byte line of a row
   __shared__ float4 stage[CH][kRegThreads];
   const int lane = threadIdx.x;
@@ -658,10 +688,10 @@ struct CodeRT {
   int K, gen;
   uint64_t poly[3];
 };
-template <int NP, bool HARD>
+template <int NP, bool HARD, bool F32 = false>
 __global__ __launch_bounds__(kRegThreads) void channel_frames_rt(ChanArgs a, CodeRT code) {
   constexpr CodeSpec C{NP, 3, {0, 0, 0, 0, 0, 0, 0, 0}, GEN_REF_X86};   // n only: the encoder is RT
-  using Src = ChannelSource<C, HARD, EncoderRT<NP>>;
+  using Src = ChannelSource<C, HARD, EncoderRT<NP>, F32>;
   using MT = typename Src::MT;
   const int b = blockIdx.x * kRegThreads + threadIdx.x;
   if (b >= a.r.nblocks) return;
@@ -680,12 +710,12 @@ __global__ __launch_bounds__(kRegThreads) void channel_frames_rt(ChanArgs a, Cod
 
 // K = 8, 9: multilane kernel (acs_multi.hpp); every lane of a block's group generates the block's
 // input (the same draws), lane q = 0 owns the info and export writes.
-template <CodeSpec C, bool HARD>
+template <CodeSpec C, bool HARD, bool F32 = false>
 __global__ __launch_bounds__(kRegThreads) void viterbi_channel_multi(ChanArgs a) {
   using X = Multi<C>;
   constexpr int NS = X::NS;
   constexpr int n = X::n;
-  using Src = ChannelSource<C, HARD>;
+  using Src = ChannelSource<C, HARD, Encoder<C>, F32>;
   using MT = typename Src::MT;
   const int lane = threadIdx.x;
   const int q = lane & (X::L - 1);

@@ -1,0 +1,78 @@
+// reg_channel.hpp -- launch templates of the channel-fused decode kernels (channel_dev.hpp), shared
+// by reg_channel.hip (BSC, and AWGN with the double-precision Box-Muller) and reg_channel_f32.hip
+// (AWGN with the opt-in fp32 Box-Muller): two translation units so they compile in parallel.
+#pragma once
+#include <array>
+#include <utility>
+
+#include "channel_dev.hpp"
+#include "reg_codes.hpp"
+
+namespace ccv {
+namespace chan_impl {
+
+// LDS budget of the decision column array per wave (opt-in kernel): 20 KiB = 8 waves per CU
+constexpr size_t kChanLdsBudget = 20 * 1024;
+
+template <size_t I, bool HARD, bool F32>
+hipError_t launch_reg(const ChanArgs& a, int grid, hipStream_t stream) {
+  constexpr CodeSpec C = kRegCodes[I];
+  constexpr size_t word = (1u << (C.K - 1)) > 32 ? 8 : 4;
+  const size_t lds = (size_t)(a.r.T - (C.K - 1)) * word * kRegThreads;
+  if (!a.global_decisions && lds <= kChanLdsBudget)
+    hipLaunchKernelGGL((viterbi_channel_lds<C, HARD, F32>), dim3(grid), dim3(kRegThreads), lds, stream, a);
+  else
+    hipLaunchKernelGGL((viterbi_channel_reg<C, HARD, F32>), dim3(grid), dim3(kRegThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <size_t I, bool HARD, bool F32>
+hipError_t launch_multi(const ChanArgs& a, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL((viterbi_channel_multi<kMultiCodes[I], HARD, F32>), dim3(grid), dim3(kRegThreads), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+template <size_t I, bool F32>
+hipError_t launch_frames(const ChanArgs& a, int grid, hipStream_t stream) {
+  if constexpr (kMultiCodes[I].n == 2) {
+    hipLaunchKernelGGL((channel_frames<kMultiCodes[I], false, F32>), dim3(grid), dim3(kRegThreads), 0, stream, a);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+
+template <bool HARD, bool F32>
+hipError_t launch_frames_rt(const ChanArgs& a, int n, const CodeRT& code, hipStream_t stream) {
+  const dim3 grid((unsigned)((a.r.nblocks + kRegThreads - 1) / kRegThreads)), block(kRegThreads);
+  switch (n) {
+    case 1: hipLaunchKernelGGL((channel_frames_rt<1, HARD, F32>), grid, block, 0, stream, a, code); break;
+    case 2: hipLaunchKernelGGL((channel_frames_rt<2, HARD, F32>), grid, block, 0, stream, a, code); break;
+    case 3: hipLaunchKernelGGL((channel_frames_rt<3, HARD, F32>), grid, block, 0, stream, a, code); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <bool HARD, bool F32, size_t... I>
+constexpr std::array<ChanLaunchFn, sizeof...(I)> make_reg(std::index_sequence<I...>) {
+  return {&launch_reg<I, HARD, F32>...};
+}
+template <bool HARD, bool F32, size_t... I>
+constexpr std::array<ChanLaunchFn, sizeof...(I)> make_multi(std::index_sequence<I...>) {
+  return {&launch_multi<I, HARD, F32>...};
+}
+template <bool F32, size_t... I>
+constexpr std::array<ChanLaunchFn, sizeof...(I)> make_frames(std::index_sequence<I...>) {
+  return {&launch_frames<I, F32>...};
+}
+
+}  // namespace chan_impl
+
+// reg_channel_f32.hip: the fp32-noise AWGN launchers ([kNumRegCodes] / [kNumMultiCodes])
+const ChanLaunchFn* channel_launchers_f32(bool multi);
+const ChanLaunchFn* channel_frames_launchers_f32();
+hipError_t launch_channel_frames_rt_f32(const ChanArgs& a, int n, const CodeRT& code, hipStream_t stream);
+
+}  // namespace ccv
