@@ -947,18 +947,21 @@ def test_device_channel_warm_up_changes_nothing(torch_cuda, decoder, c, channel)
     assert warm(point, 5 << 40, 9000) == want
 
 
+@pytest.mark.parametrize("noise_f32", [False, True], ids=["f64", "f32"])
 @pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["ref", "true"])
-def test_device_channel_k9_frames_path_equals_fused(torch_cuda, gen):
+def test_device_channel_k9_frames_path_equals_fused(torch_cuda, gen, noise_f32):
     """K = 9 soft at blen 40: ccv_simulate_device writes the frames (channel_frames) and decodes them
     with the persistent kernel (x86 idiom: one lane per block; true parity: two lanes); the fused
     multilane channel kernel (option channel_fused=1) draws the same frames -- info, decoder input,
-    output and error count are identical, with and without the hard demapper, for ragged batches."""
+    output and error count are identical, with and without the hard demapper, for ragged batches,
+    in both noise modes."""
     c = K9.with_(gen_mode=gen)
     for nb, hard_demap in ((1, False), (200, False), (3 * 64 + 5, True)):
         runs = []
         for fused in (0, 1):
             runs.append(_simulate(torch_cuda, Plan(c, SOFT).set_option("channel_fused", fused), c, 21,
-                                  7000 + nb, nb, ch.noise_scaling(2.0), hard_demap=hard_demap))
+                                  7000 + nb, nb, ch.noise_scaling(2.0), hard_demap=hard_demap,
+                                  noise_f32=noise_f32))
         a, b = runs
         for k in (0, 1, 2):
             assert np.array_equal(a[k], b[k])
@@ -1004,17 +1007,18 @@ def test_device_channel_frames_only(torch_cuda, idx, channel):
     plan.close()
 
 
-@pytest.mark.parametrize("channel", [SOFT, HARD])
-def test_device_channel_lds_vs_hbm_decisions(torch_cuda, channel):
+@pytest.mark.parametrize("channel,noise_f32", [(SOFT, False), (SOFT, True), (HARD, False)],
+                         ids=["soft", "soft_f32", "hard"])
+def test_device_channel_lds_vs_hbm_decisions(torch_cuda, channel, noise_f32):
     """The LDS-decision channel kernel (option channel_lds_decisions=1, the BSC default) and the
     HBM-scratch one (=0, the AWGN default) decode the same device-generated frames identically
-    (outputs, path metrics, error counts)."""
+    (outputs, path metrics, error counts), in both noise modes."""
     param = 70000 if channel == HARD else ch.noise_scaling(1.0)
     for c in (K7, CODEBOOK[0], CODEBOOK[3].with_(blen=80), K7.with_(blen=1)):
         runs = []
         for forced in (1, 0):
             plan = Plan(c, channel).set_option("channel_lds_decisions", forced)
-            runs.append(_simulate(torch_cuda, plan, c, 3, 5000, 777, param))
+            runs.append(_simulate(torch_cuda, plan, c, 3, 5000, 777, param, noise_f32=noise_f32))
         a, b = runs
         for x, y in zip(a[:4], b[:4]):
             if channel == SOFT and x is a[3]:
