@@ -586,12 +586,9 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   using Src = ChannelSource<C, HARD, Encoder<C>, F32>;
   using SM = typename Src::MT;                                      // source metric type
   // ACS metric type: uint16_t for the BSC (fp32, exact here as in the persistent BSC kernel,
-  // acs_persist.hpp, measured 1 % slower in this kernel, whose time is the channel's: 108.7-109.7 vs
-  // 110.1-111.0 Gbit/s with u16, profiles/r05d/)
-#ifndef CCV_CHAN_BSC_F32
-#define CCV_CHAN_BSC_F32 0
-#endif
-  using MT = typename std::conditional<HARD && !CCV_CHAN_BSC_F32, uint16_t, float>::type;
+  // acs_persist.hpp, measured 1 % slower in this kernel, whose time is the channel's, and mixed
+  // after the unrolled loop: profiles/r05d/, profiles/r05_chan/chan_bench_bsc_f32_ab.jsonl)
+  using MT = typename std::conditional<HARD, uint16_t, float>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char chan_lds[];
   DW* dl = reinterpret_cast<DW*>(chan_lds);
   const int lane = threadIdx.x;
