@@ -52,7 +52,7 @@ struct ChanArgs {
   int hard_demap;            // AWGN: common/hard-demapper.c instead of common/demapper.c
   uint8_t* info_out;         // [nb][IB] transmitted info bytes (required)
   void* ch_out;              // optional export: soft float [nb][T][2^n] / hard uint8 [nb][T]
-  int global_decisions;      // K <= 7: decisions through r.dec in HBM instead of LDS (A/B, long T)
+  int global_decisions;      // K <= 7: 1 decisions through r.dec in HBM, 0 in LDS, -1 by occupancy
   int noise_f32;             // AWGN: the fp32 Box-Muller (CCV_CHANNEL_NOISE_F32, opt-in) instead of double
 };
 

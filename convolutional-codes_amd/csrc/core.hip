@@ -1047,12 +1047,12 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   if (hard && a.noise_f32) return fail("the fp32 Box-Muller belongs to the AWGN channel");
   a.info_out = d_info;
   a.ch_out = d_channel;
-  // Decisions in LDS (viterbi_channel_lds) for BSC, in HBM scratch for AWGN: the 20 KiB column per
-  // wave caps a CU at 8 waves; the BSC kernel gains more from the saved decision traffic (108.6 vs
-  // 96.6 Gbit/s at K=7), the double-precision AWGN kernel loses more occupancy than it saves (60.3
-  // vs 62.5). Option "channel_lds_decisions" 1 / 0 forces either (A/B).
-  const bool lds_dec = p->opt.channel_lds_decisions < 0 ? hard : p->opt.channel_lds_decisions != 0;
-  a.global_decisions = (p->global_decisions || !lds_dec) ? 1 : 0;
+  // K <= 7 decisions in LDS (viterbi_channel_lds) or in HBM scratch (viterbi_channel_reg): the LDS
+  // column (20 KiB per wave at K = 7) caps a CU's waves; by default the launch compares the two
+  // kernels' occupancy (reg_channel.hpp). Option "channel_lds_decisions" 1 / 0 forces either (A/B).
+  a.global_decisions = p->global_decisions ? 1
+                       : p->opt.channel_lds_decisions < 0 ? -1
+                                                          : (p->opt.channel_lds_decisions != 0 ? 0 : 1);
   if (frames_path) {
     void* frames = d_channel;
     if (!frames) {

@@ -14,12 +14,28 @@ namespace chan_impl {
 // LDS budget of the decision column array per wave (opt-in kernel): 20 KiB = 8 waves per CU
 constexpr size_t kChanLdsBudget = 20 * 1024;
 
+// Waves per CU of a one-wave-workgroup kernel with `lds` bytes of dynamic LDS.
+inline int waves_per_cu(const void* fn, size_t lds) {
+  int n = 0;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kRegThreads, lds) == hipSuccess ? n : 0;
+}
+
+// Decisions in LDS only where that costs no occupancy: LDS when its kernel holds at least as many
+// waves per CU as the HBM-scratch one. Measured (profiles/r05_chan/chan_bench_lds_ab.jsonl, both
+// forced and auto): K = 7 BSC idiom HBM 147 vs LDS 127 Gbit/s, BSC true parity (8 vs 8 waves) LDS
+// 107 vs 99, code 3 BSC HBM 194 vs 188, code 0 AWGN fp32 HBM 366 vs 326; every AWGN kernel HBM.
 template <size_t I, bool HARD, bool F32>
 hipError_t launch_reg(const ChanArgs& a, int grid, hipStream_t stream) {
   constexpr CodeSpec C = kRegCodes[I];
   constexpr size_t word = (1u << (C.K - 1)) > 32 ? 8 : 4;
   const size_t lds = (size_t)(a.r.T - (C.K - 1)) * word * kRegThreads;
-  if (!a.global_decisions && lds <= kChanLdsBudget)
+  bool use_lds = a.global_decisions != 1 && lds <= kChanLdsBudget;
+  if (use_lds && a.global_decisions < 0) {
+    const int w_lds = waves_per_cu(reinterpret_cast<const void*>(&viterbi_channel_lds<C, HARD, F32>), lds);
+    const int w_reg = waves_per_cu(reinterpret_cast<const void*>(&viterbi_channel_reg<C, HARD, F32>), 0);
+    use_lds = w_lds >= w_reg;
+  }
+  if (use_lds)
     hipLaunchKernelGGL((viterbi_channel_lds<C, HARD, F32>), dim3(grid), dim3(kRegThreads), lds, stream, a);
   else
     hipLaunchKernelGGL((viterbi_channel_reg<C, HARD, F32>), dim3(grid), dim3(kRegThreads), 0, stream, a);

@@ -1010,8 +1010,8 @@ def test_device_channel_frames_only(torch_cuda, idx, channel):
 @pytest.mark.parametrize("channel,noise_f32", [(SOFT, False), (SOFT, True), (HARD, False)],
                          ids=["soft", "soft_f32", "hard"])
 def test_device_channel_lds_vs_hbm_decisions(torch_cuda, channel, noise_f32):
-    """The LDS-decision channel kernel (option channel_lds_decisions=1, the BSC default) and the
-    HBM-scratch one (=0, the AWGN default) decode the same device-generated frames identically
+    """The LDS-decision channel kernel (option channel_lds_decisions=1) and the HBM-scratch one (=0;
+    -1, the default, picks by occupancy) decode the same device-generated frames identically
     (outputs, path metrics, error counts), in both noise modes."""
     param = 70000 if channel == HARD else ch.noise_scaling(1.0)
     for c in (K7, CODEBOOK[0], CODEBOOK[3].with_(blen=80), K7.with_(blen=1)):

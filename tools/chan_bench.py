@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--chunks", type=int, default=8)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="plan option (ccv_plan_set_option), e.g. channel_lds_decisions=0")
     args = ap.parse_args()
     import torch
     for name in args.code:
@@ -28,6 +30,9 @@ def main():
         channel, point = (HARD, args.bsc) if args.bsc is not None else (SOFT, args.ebn0)
         for nz in (["-"] if channel == HARD else args.noise):
             dev = DeviceChannelDecoder(code, channel, 25000, 0xC0DE, noise_f32=nz == "f32")
+            for opt in args.option:
+                oname, value = opt.split("=")
+                dev.plan.set_option(oname, int(value))
             dev.warm_up(0.3, point)
             nb = dev.chunk * args.chunks
             rates = []
@@ -36,7 +41,7 @@ def main():
                 t0 = time.perf_counter()
                 dev(point, r * nb, nb)   # syncs (reads the error count)
                 rates.append(nb * code.blen / (time.perf_counter() - t0) / 1e9)
-            print(json.dumps({"tag": args.tag, "code": name, "noise": nz, "point": point,
+            print(json.dumps({"tag": args.tag, "options": args.option, "code": name, "noise": nz, "point": point,
                               "bits": nb * code.blen, "best_gbit_s": round(max(rates), 2),
                               "median_gbit_s": round(statistics.median(rates), 2)}), flush=True)
 
