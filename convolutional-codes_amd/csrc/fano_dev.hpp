@@ -106,6 +106,12 @@ constexpr int kFanoTimeoutPerBit = 10000;   // fano-decoder.c:14
 // per node in LDS: 9 -> 11 waves per CU at K = 15, but the mask updates cost more than the occupancy
 // gained -- 67 -> 60 Mbit/s soft, 222 -> 218 BSC, profiles/r05c/ab/fanoreg*.)
 constexpr int kFanoThreads = 64;
+// LDS bytes of the node arrays (metrics [T + 1][64] + a flags byte per node), 16-byte aligned; the
+// rows follow. (Round 5 measured 2-bit packed flags -- 9 -> 10 waves per CU, updates by two LDS
+// atomics: 67.3 -> 64.5 Mbit/s soft, 217 -> 209 BSC, profiles/r05_fano/.)
+__host__ __device__ constexpr size_t fano_node_bytes(int T, size_t metric_bytes) {
+  return ((size_t)(T + 1) * kFanoThreads * (metric_bytes + 1) + 15) & ~(size_t)15;
+}
 
 // Received-symbol access per lane (RM):
 //   kRowsDirect: the branch metrics of the node a move lands on read r[e] from global memory after
@@ -161,7 +167,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   MT* metric = reinterpret_cast<MT*>(smem);
   uint8_t* flags = smem + (size_t)(T + 1) * kFanoThreads * sizeof(MT);   // sel | dec << 1
   // rows: [T][64] float4 (soft) or bytes (hard), after the flags (16-byte aligned)
-  unsigned char* rows = smem + (((size_t)(T + 1) * kFanoThreads * (sizeof(MT) + 1) + 15) & ~(size_t)15);
+  unsigned char* rows = smem + fano_node_bytes(T, sizeof(MT));
   // a node's flags byte (sel | dec << 1)
   auto flag_get = [&](int d) -> uint32_t { return flags[d * kFanoThreads + lane]; };
   // store v at node d when `write`; otherwise into the spare row T (branch-free)

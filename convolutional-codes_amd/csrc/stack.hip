@@ -171,7 +171,7 @@ static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream
 // (16 B per node) cut the chip from 9 to 2 waves per CU and run 4x slower. The plan option
 // "fano_rows" (FanoArgs::rows_mode) overrides.
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
-  const size_t node_bytes = ((size_t)(a.T + 1) * kFanoThreads * ((hard ? sizeof(int32_t) : sizeof(float)) + 1) + 15) & ~(size_t)15;
+  const size_t node_bytes = fano_node_bytes(a.T, hard ? sizeof(int32_t) : sizeof(float));
   const size_t row_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : 16);
   const bool rowable = hard || (a.n == 2 && a.K <= 32);
   int rm = hard ? kRowsLds : (rowable ? kRowsGlobal : kRowsDirect);
