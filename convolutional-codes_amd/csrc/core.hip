@@ -1020,11 +1020,12 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
     if (p->sim_out.grow(nblocks * (size_t)p->d.out_bytes, stream)) return -1;
     d_out = static_cast<uint8_t*>(p->sim_out.ptr);
   }
-  // K = 9 soft at blen 40: frames to HBM once per block, then the persistent decode (x86 idiom: one
-  // lane per block, acs_wide.hpp; true parity: acs_multi.hpp) with the fused error count -- the
-  // multilane channel kernel draws every block's channel once per lane of its four-lane group
-  const bool frames_path = !hard && p->multi_index >= 0 && persist_kernel(*p, false) != nullptr &&
-                           !p->opt.channel_fused;
+  // K = 8, 9: frames to HBM once per block, then the decode with the fused error count (soft at
+  // blen 40: the persistent kernels, acs_wide.hpp / acs_multi2.hpp; BSC: the multilane kernel, its
+  // input one byte per step) -- the fused multilane channel kernel draws every block's channel once
+  // per lane of its group (option channel_fused 1 keeps it)
+  const bool frames_path = p->multi_index >= 0 && !p->opt.channel_fused && !p->step_major &&
+                           (hard || persist_kernel(*p, false) != nullptr);
   if (!frames_path && p->dec.grow(decision_bytes(*p, nblocks), stream)) return -1;
   ccv::ChanArgs a{};
   a.r.in = nullptr;
@@ -1060,9 +1061,13 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
       frames = p->sim_frames.ptr;
     }
     a.ch_out = frames;
-    HIP_TRY(ccv::channel_frames_launchers()[p->multi_index](
-        a, (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads), stream));
-    return ccv_decode_device(p, frames, nblocks, d_out, nullptr, d_info, d_errors, nullptr, stream_v);
+    if (hard)
+      HIP_TRY(ccv::launch_channel_frames_any(a, p->d.n, p->d.K, p->polys, p->d.gen_mode, true, stream));
+    else
+      HIP_TRY(ccv::channel_frames_launchers()[p->multi_index](
+          a, (int)((nblocks + ccv::kRegThreads - 1) / ccv::kRegThreads), stream));
+    return ccv_decode_device(p, frames, nblocks, d_out, hard ? d_path_metric : nullptr, d_info, d_errors,
+                             nullptr, stream_v);
   }
   const int grid = (int)(padded_columns(*p, nblocks) / ccv::kRegThreads);
   const bool multi = p->reg_index < 0;
