@@ -375,6 +375,10 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="plan option (ccv_plan_set_option, include/ccv.h) for A/B runs; repeatable")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
+                    help="process-group backend for N > 1 (default nccl = RCCL over xGMI)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on cuda:0, reductions over gloo")
     ap.add_argument("--no-hbm-probe", action="store_true",
                     help="skip the achievable-HBM probe (A/B runs of builds that predate it)")
     ap.add_argument("--no-fused-channel", action="store_true",
@@ -396,9 +400,17 @@ def main(argv=None):
     from ccviterbi import HARD, SOFT, FanoPlan, Plan, StackPlan, channel as ch, named_code
     from ccviterbi.decoder import FLAG_GLOBAL_DECISIONS, FLAG_NO_PERSISTENT, FLAG_STEP_MAJOR
 
-    torch.cuda.set_device(local_rank)
+    # --same-device (a multi-process rehearsal on a one-GPU box): every rank on cuda:0, the
+    # reductions over gloo (RCCL refuses two ranks on one device); the production form is one rank
+    # per GPU over RCCL
+    device_index = 0 if args.same_device else local_rank
+    backend = args.backend or ("gloo" if args.same_device else "nccl")
+    torch.cuda.set_device(device_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
+        else:
+            dist.init_process_group("gloo")
 
     stack = args.decoder == "stack"
     sequential = args.decoder != "viterbi"
@@ -523,7 +535,8 @@ def main(argv=None):
     errors = int(errs.item())
     per_rank_kernel_ms = [round(kernel_ms, 4)]
     if world > 1:   # MAX of the timings, SUM of the error counters (RCCL over xGMI)
-        wall, kernel_ms, per_rank_kernel_ms, errors = reduce_over_ranks(dist, wall, kernel_ms, errors, "cuda")
+        wall, kernel_ms, per_rank_kernel_ms, errors = reduce_over_ranks(
+            dist, wall, kernel_ms, errors, "cuda" if backend == "nccl" else "cpu")
     bits_per_step = world * nb * code.blen
 
     if rank == 0:
@@ -600,6 +613,8 @@ def main(argv=None):
                 "channel": args.channel,
                 **({"p_ppm": args.p_ppm} if hard else {"ebn0_db": args.ebn0}),
                 "parallelism": f"dp{world} (frames sharded, counters all-reduced once)",
+                "backend": backend if world > 1 else None,
+                "same_device_rehearsal": bool(args.same_device),
                 "kernel": plan.kernel,
                 "variant": getattr(plan, "variant", plan.kernel),
                 **({"options": dict(o.split("=", 1) for o in args.option)} if args.option else {}),

@@ -312,6 +312,8 @@ def main(argv=None, decode=None):
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); self-launches torchrun")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
                     help="process-group backend (default nccl = RCCL over xGMI)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on cuda:0 (use with --backend gloo)")
     ap.add_argument("--out", default=None, help="also write the points as a JSON list (rank 0)")
     ap.add_argument("--warmup", type=float, default=0.2,
                     help="seconds of throw-away device-channel chunks before the first point (allocation, "
@@ -338,11 +340,12 @@ def main(argv=None, decode=None):
 
     import torch
     import torch.distributed as dist
+    device_index = 0 if args.same_device else local_rank
     if backend == "nccl" or decode is None:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(device_index)
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
         else:
             dist.init_process_group("gloo")
 
