@@ -401,6 +401,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     walk_period.template operator()<1>();
     const uint64_t bits = __builtin_bitreverse64(h);   // bit 63 - t = output of step t
     if (q == 0 && blk < nb) {
+      if (a.path_metric) a.path_metric[blk] = (int32_t)mn;   // BSC input through Hamming rows
       uint8_t* o = a.out + (size_t)blk * OB;
 #pragma unroll
       for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));

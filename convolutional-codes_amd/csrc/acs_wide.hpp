@@ -173,9 +173,9 @@ __device__ __forceinline__ void growth_step_wide(float (&M)[1 << (C.K - 1)], con
 // Lowest-index minimum over S > 64 states (acs_reg.hpp argmin_state: v_min3 tree, per state the sign
 // of mn - M[s] into a "differs" mask, lowest clear bit).
 template <int S>
-__device__ __forceinline__ uint32_t argmin_wide(const float (&M)[S]) {
+__device__ __forceinline__ uint32_t argmin_wide(const float (&M)[S], float& mn) {
   constexpr int W = S / 32;
-  const float mn = tree_min<S, float>(M);
+  mn = tree_min<S, float>(M);
   uint32_t idx = 0;
 #pragma unroll
   for (int w = W - 1; w >= 0; --w) {   // the lowest word with a minimum wins
@@ -353,7 +353,11 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
     // Traceback (reference :71-90) from the lowest-index minimum. The history word h starts as the
     // final state (its bits are the outputs of the last K-1 steps) and takes the decision of main
     // step m (the output of step m) at the bottom; its low K-1 bits are always the current state.
-    uint64_t h = argmin_wide<S>(M);
+    float best;
+    uint64_t h = argmin_wide<S>(M, best);
+    // BSC input (ccv_decode_device converts its symbols to Hamming-distance rows): the path metric
+    // (binary-symmetric-channel/viterbi-decoder.c:95), a small integer, exact in fp32
+    if (a.path_metric && b < nb) a.path_metric[b] = (int32_t)best;
     // The decision words come back in quarters of the block, two quarters in flight: a quarter is
     // walked while the next one loads. The group's stores are drained first (vmcnt(0): L2 has
     // acknowledged them) and the loads are agent-scope (sc1), so they miss the CU's L1, which may

@@ -135,6 +135,7 @@ struct ccv_plan {
   bool generic_ok = false;                     // the generic kernel can run this code (d_exp built)
   DeviceBuffer sim_info, sim_out;             // ccv_simulate_device scratch (caller passed none)
   DeviceBuffer sim_frames;                    // ccv_simulate_device: K = 9 frames ahead of the wide decode
+  DeviceBuffer hard_rows;                     // K = 9 BSC: the symbols as Hamming-distance rows (hard_rows)
   hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
   // ccv_plan_set_option (include/ccv.h): kernel A/B switches per plan; defaults = production paths
   struct Options {
@@ -183,11 +184,25 @@ ccv::RegLaunchFn regdec_kernel(const ccv_plan& p, bool export_decisions) {
 // The persistent K = 9 soft kernel with a per-wave decision slot (acs_wide.hpp one lane per block for
 // the x86-idiom code, acs_multi2.hpp viterbi_multi2_slot two lanes per block for true parity), or
 // nullptr: codebook block length, block-major input, decisions not exported.
+// (BSC plans too: ccv_decode_device first turns their symbols into Hamming-distance rows, hard_rows)
 ccv::RegLaunchFn wide_kernel(const ccv_plan& p, bool export_decisions) {
   if (p.no_persistent || p.global_decisions || export_decisions || p.step_major ||
-      p.d.blen != ccv::kPersistBlen || p.multi_index < 0 || p.d.channel != CCV_SOFT)
+      p.d.blen != ccv::kPersistBlen || p.multi_index < 0 || p.d.n != 2)
     return nullptr;
   return ccv::multi_wide_launchers()[p.multi_index];
+}
+
+// BSC symbols -> the soft K = 9 persistent kernels' input rows: entry k = popcount(k ^ (sym & 3)),
+// the Hamming branch metric of expected symbol k (binary-symmetric-channel/viterbi-decoder.c:69-72,
+// the symbol masked as at :237). Their fp32 metrics are exact on these small integers, and the
+// reference's 0xFF00 saturation only binds at the growth steps' unreachable states, where it and the
+// soft kernels' +inf give the same decisions.
+__global__ __launch_bounds__(256) void hard_rows(const uint8_t* __restrict__ in, float4* __restrict__ out, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const uint32_t s = in[i] & 3u;
+    out[i] = make_float4((float)__builtin_popcount(s), (float)__builtin_popcount(s ^ 1u),
+                         (float)__builtin_popcount(s ^ 2u), (float)__builtin_popcount(s ^ 3u));
+  }
 }
 
 // The persistent kernel (acs_persist.hpp K <= 7, acs_wide.hpp / acs_multi2.hpp K = 9), or nullptr:
@@ -532,6 +547,7 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->sim_info.release();
   p->sim_out.release();
   p->sim_frames.release();
+  p->hard_rows.release();
   p->counter.release();
   p->symtab.release();
   p->order.release();
@@ -653,6 +669,15 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
       // (four lanes per block, acs_multi.hpp viterbi_multi_slot) blocks
       if (grow_wide_scratch(*p, wide, stream)) return -1;
       a.dec = p->dec.ptr;
+      if (hard) {
+        const size_t n = nblocks * (size_t)p->d.steps;
+        if (p->hard_rows.grow(n * sizeof(float4), stream)) return -1;
+        const size_t grid = std::min<size_t>((n + 255) / 256, 8192);
+        hipLaunchKernelGGL(hard_rows, dim3((unsigned)grid), dim3(256), 0, stream,
+                           static_cast<const uint8_t*>(d_in), static_cast<float4*>(p->hard_rows.ptr), n);
+        HIP_TRY(hipGetLastError());
+        a.in = p->hard_rows.ptr;
+      }
       const size_t gb = (size_t)ccv::multi_wide_group_blocks(p->multi_index);
       HIP_TRY(wide(a, (int)((nblocks + gb - 1) / gb), stream));
       return 0;

@@ -454,6 +454,26 @@ def test_k9_wide_kernel(torch_cuda, nb, gen):
 
 
 
+@pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["ref", "true"])
+def test_k9_bsc_through_the_persistent_kernels(torch_cuda, gen):
+    """K = 9 BSC at blen 40 runs the soft persistent kernels on Hamming-distance rows (core.hip
+    hard_rows; x86 idiom: one lane per block, true parity: two lanes): outputs and path metrics equal
+    the oracle's and the multilane BSC kernel's, for ragged batches, from clean to p = 0.4 (where the
+    0xFF00 saturation of the reference would show if it mattered)."""
+    c = K9.with_(gen_mode=gen)
+    plan = Plan(c, HARD)
+    assert plan.variant == ("persistent-wide" if gen == GEN_REF_X86 else "persistent-slot2")
+    multilane = Plan(c, HARD, FLAG_NO_PERSISTENT)
+    assert multilane.variant.startswith("multilane")
+    for nb, p_ppm in ((1, 0), (3 * 64 + 5, 50000), (2048 + 77, 400000)):
+        _, syms = ch.bsc_blocks(c, nb, p_ppm, 1234 + nb)
+        out, pm = plan.decode_host(syms)
+        ref, ref_pm = O.viterbi_hard(_ocode(c), syms)
+        assert np.array_equal(out, ref) and np.array_equal(pm, ref_pm)
+        out2, pm2 = multilane.decode_host(syms)
+        assert np.array_equal(out, out2) and np.array_equal(pm, pm2)
+
+
 def test_k9_true_two_lane_kernel_ragged_groups(torch_cuda):
     """The true-parity K = 9 kernel (two lanes per block, acs_multi2.hpp) decodes a ragged batch of
     several rounds of 32-block groups over the resident waves identically to the oracle."""
