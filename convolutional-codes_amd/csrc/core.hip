@@ -148,7 +148,7 @@ struct ccv_plan {
     int fano_order = 1;              // soft: noisiest first
     long long fano_cap = -1;         // -1 default 4000 x T, 0 one pass
     int fano_count_moves = 0;        // diagnostics: iterations = moves
-    int channel_fused = 0;           // K = 9 soft device channel: fused multilane kernel
+    int channel_fused = 0;           // K = 8 / 9 device channel: fused multilane kernel
     int channel_lds_decisions = -1;  // device channel K <= 7: -1 auto (BSC LDS, AWGN HBM), 0, 1
   } opt;
 };

@@ -201,7 +201,7 @@ int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out
  *                 "fano_cap"         -1 default (4000 x T moves), 0 one pass, else moves before parking
  *                 "fano_count_moves" 1: d_iterations gets moves instead of timeout ticks (diagnostics)
  *   Viterbi plans (on-device channel):
- *                 "channel_fused"    1: K = 9 soft codes use the fused multilane channel kernel
+ *                 "channel_fused"    1: K = 8 / 9 codes use the fused multilane channel kernel
  *                 "channel_lds_decisions"  -1 auto (LDS unless it costs occupancy), 0 HBM, 1 LDS (K <= 7) */
 int ccv_plan_set_option(ccv_plan* plan, const char* name, long long value);
 
