@@ -41,6 +41,7 @@ if has bench; then
   run k9 300 --code k9 --frames 32                               # config 3 (port + AVX2 baselines)
   run k7_true 300 --code k7:true                                 # textbook (171,133)
   run k9_true 300 --code k9:true --frames 32                     # textbook (561,753)
+  run k9_bsc 300 --code k9 --channel bsc --frames 32             # K = 9 BSC (soft kernel on Hamming rows)
   run stack 300 --decoder stack --frames 16 --steps 5 --warmup 1  # config 5 (16 frames: DESIGN 4.5)
   run stack_bsc 300 --decoder stack --channel bsc --frames 16 --steps 5 --warmup 1
   run fano 900 --decoder fano --steps 3 --warmup 1               # bounded reference-decoder sample
