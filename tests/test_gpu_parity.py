@@ -91,10 +91,11 @@ def test_register_kernel_selected_for_benchmark_codes():
     assert Plan(K7, SOFT, FLAG_GENERIC).decisions == "lds"          # acs_generic.hpp
     # K = 8, 9 (multilane kernel): register-resident up to T = 48 (K9) / 49 (K8), soft and hard
     for c in (K8, K9, K9.with_(gen_mode=GEN_TRUE_PARITY)):
-        # the K = 9 x86-idiom soft code runs one lane per block with a per-wave decision slot
-        # (the true-parity K = 9 code two lanes per block with a slot too, viterbi_multi2_slot)
-        soft = "slot" if c.K == 9 else "registers"
-        assert Plan(c, SOFT).decisions == soft and Plan(c, HARD).decisions == "registers"
+        # the K = 9 x86-idiom code runs one lane per block with a per-wave decision slot (the
+        # true-parity K = 9 code two lanes per block with a slot too, viterbi_multi2_slot); the BSC
+        # at K = 9 runs the same kernels on Hamming-distance rows
+        slot = "slot" if c.K == 9 else "registers"
+        assert Plan(c, SOFT).decisions == slot and Plan(c, HARD).decisions == slot
         assert Plan(c, SOFT, FLAG_GLOBAL_DECISIONS).decisions == "hbm"
         assert Plan(c, SOFT, FLAG_NO_PERSISTENT).decisions == "registers"
     assert Plan(K9.with_(blen=41), SOFT).decisions == "hbm"           # T = 49
