@@ -182,19 +182,31 @@ struct Constellation<3> {
 // at bit 63 - j), so a whole word of it is the XOR of the info word shifted right by each tap j
 // (funnelled with the previous word), computed once per 32 steps; the x86 idiom (GEN_REF_X86: the
 // result cleared when the taps at register bits 4 mod 8 have odd parity) is one more such XOR. Per
-// step: the symbol's bits are the streams' top bits, then one shift each. The info window w[0..7]
-// holds the bits MSB-first, cleared from blen on (the tail steps shift in zeros).
-template <CodeSpec C>
+// step: the symbol's bits are the streams' top bits, then one shift each. The info bits are MSB-first,
+// cleared from blen on (the tail steps shift in zeros); init assembles all eight window words in
+// w[0..7], start() keeps the current and the next word in registers and parks words 2..7 in LDS
+// (6 words x 64 lanes), read back one per 32 steps, a whole word period before they are needed
+// (~10 fewer VGPRs; the LDS-decision kernel, whose occupancy is set by its LDS, keeps them in
+// registers).
+template <CodeSpec C, bool PARK = true>   // PARK false: the whole window stays in registers
 struct Encoder {
   static_assert(C.K >= 2 && C.K <= 32, "bit-sliced encoder: taps within one word");
-  uint32_t w[8];
+  uint32_t w[8];     // init: the whole window; PARK: from start() on only w[0] (current), w[1] (next)
   uint32_t e[C.n];   // stream k of the current 32-step word, the current step in bit 31
   int t;
+  __device__ __forceinline__ static uint32_t* park() {   // this lane's column of words 2..7, [6][64]
+    __shared__ uint32_t parked[6 * kRegThreads];
+    return parked + threadIdx.x;
+  }
   __device__ __forceinline__ void start(int blen) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int valid = blen - 32 * k;
       w[k] &= valid >= 32 ? ~0u : (valid <= 0 ? 0u : ~0u << (32 - valid));
+    }
+    if constexpr (PARK) {
+#pragma unroll
+      for (int k = 2; k < 8; ++k) park()[(k - 2) * kRegThreads] = w[k];
     }
     t = 0;
     fill(0u, w[0]);
@@ -228,9 +240,16 @@ struct Encoder {
     ++t;
     if ((t & 31) == 0) {
       const uint32_t prev = w[0];
+      if constexpr (PARK) {
+        w[0] = w[1];
+        const int next = (t >> 5) - 1;   // words 2, 3, ... come in at t = 32, 64, ...
+        const uint32_t nw = park()[(next < 6 ? next : 5) * kRegThreads];
+        w[1] = next < 6 ? nw : 0u;
+      } else {
 #pragma unroll
-      for (int k = 0; k < 7; ++k) w[k] = w[k + 1];
-      w[7] = 0;
+        for (int k = 0; k < 7; ++k) w[k] = w[k + 1];
+        w[7] = 0;
+      }
       fill(prev, w[0]);
       asm volatile("");
     } else {
@@ -586,7 +605,8 @@ __global__ __launch_bounds__(kRegThreads) void viterbi_channel_lds(ChanArgs a) {
   constexpr int NS = 1 << C.n;
   constexpr int G = C.K - 1;
   using DW = DecWord<S>;
-  using Src = ChannelSource<C, HARD, Encoder<C>, F32>;
+  // the encoder window stays in registers: its LDS words would cost this kernel a wave per CU
+  using Src = ChannelSource<C, HARD, Encoder<C, false>, F32>;
   using SM = typename Src::MT;                                      // source metric type
   // ACS metric type: uint16_t for the BSC (fp32, exact here as in the persistent BSC kernel,
   // acs_persist.hpp, measured 1 % slower in this kernel, whose time is the channel's, and mixed
