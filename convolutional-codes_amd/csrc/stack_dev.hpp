@@ -485,10 +485,30 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
         row_max_min<RL>(mx, mn);
         uint32_t cand = kStackDepth;
         c2 = kStackDepth;
+        if constexpr (!HARD && kRowSlots == 4) {
+          // the lane's lowest slot holding the max / min without a VCC compare-select chain: the
+          // sign of met[k] - mx (of mn - met[k]) is clear exactly on equality (+0: no metric is
+          // ever -0), shifted into a 4-bit "differs" mask whose lowest clear bit is the slot;
+          // v_ffbl gives -1 for a lane without one, above every index. -inf - -inf (a NaN, either
+          // sign) only arises with entries not on the stack: then mx = -inf (no live entry, !ok,
+          // cur unused) or mn = -inf (stack not full, c2 unused)
+          uint32_t dx = 0, dn = 0;
 #pragma unroll
-        for (int k = kRowSlots - 1; k >= 0; --k) {
-          cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
-          c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
+          for (int k = kRowSlots - 1; k >= 0; --k) {
+            dx = __builtin_amdgcn_alignbit(dx, __float_as_uint(met[k] - mx), 31);
+            dn = __builtin_amdgcn_alignbit(dn, __float_as_uint(mn - met[k]), 31);
+          }
+          uint32_t fx, fn;
+          asm("v_ffbl_b32 %0, %1" : "=v"(fx) : "v"(dx ^ 0xFu));
+          asm("v_ffbl_b32 %0, %1" : "=v"(fn) : "v"(dn ^ 0xFu));
+          cand = fx | (uint32_t)(l * kRowSlots);
+          c2 = fn | (uint32_t)(l * kRowSlots);
+        } else {
+#pragma unroll
+          for (int k = kRowSlots - 1; k >= 0; --k) {
+            cand = met[k] == mx ? (uint32_t)(l * kRowSlots + k) : cand;
+            c2 = met[k] == mn ? (uint32_t)(l * kRowSlots + k) : c2;
+          }
         }
         row_min_min_u32<RL>(cand, c2);
         cur = cand;
