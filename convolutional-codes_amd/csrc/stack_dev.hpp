@@ -419,7 +419,8 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
   const int OB = (T + 7) >> 3, IB = (a.blen + 7) >> 3;
   // record: x = next index | expected symbols (e0 << 8 | e1) << 8, y = encoder state, z/w = path
   auto symbols_of = [&](uint32_t st) -> uint32_t {
-    if constexpr (TAB) return a.symtab[st];
+    // a 32-bit byte offset from the table's SGPR base: one global_load_ushort, no 64-bit add
+    if constexpr (TAB) return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(a.symtab) + (st << 1));
     else return lane_symbols<NP, true>(poly, NP, K, idiom, (uint64_t)st);
   };
   const uint32_t esym_root = symbols_of(0);
@@ -578,7 +579,11 @@ __global__ __launch_bounds__(kStackDepth) void stack_decode_rows(StackArgs a) {
       asm volatile("" : "+v"(es));   // keeps the table load ahead of the branch below
       if (ext && l < 2) {
         ent[slot] = make_uint4((nx & 0xFFu) | (es << 8), est, p0, p1);
-        metl[slot] = dup ? lhs_met : m0;
+        // the metric's address from its own base: otherwise hipCC derives it from the record's
+        // (ent + 16 slot - 12 slot) with a 64-bit v_mad_u64_u32
+        uint32_t mslot = slot;
+        asm volatile("" : "+v"(mslot));
+        metl[mslot] = dup ? lhs_met : m0;
       }
       t = tn;
       const bool finish = bad || t > T;
