@@ -268,11 +268,16 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
     if constexpr ((ABLATE & kPersistNoDma) != 0) return;   // ablation: LDS reads of stale rows
     if constexpr ((ABLATE & kPersistCachedInput) != 0) g = blockIdx.x & 7;   // L2-resident input
     if (g * kRegThreads + kRegThreads < nb) {
-      const unsigned char* base = in + (size_t)g * kRegThreads * block_bytes + c * PF * 16;
+      // buffer form: the group's base in an SGPR descriptor, the lane's offset as the VGPR offset
+      // and the chunk's as the SGPR offset -- the global form wants a 64-bit VGPR address, one
+      // v_lshl_add_u64 ahead of every DMA, which the DMA then waits for
+      const __amdgpu_buffer_rsrc_t grp = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<unsigned char*>(in) + (size_t)g * kRegThreads * block_bytes, 0,
+          kRegThreads * block_bytes, 0x00020000);
 #pragma unroll
       for (int k = 0; k < UPR; ++k)
-        __builtin_amdgcn_global_load_lds(base + dma_off[k], (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16),
-                                         16, 0, (ABLATE & kPersistInputNt) ? 2 : 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(grp, (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16), 16,
+                                                 dma_off[k], c * PF * 16, 0, (ABLATE & kPersistInputNt) ? 2 : 0);
     } else {
 #pragma unroll
       for (int k = 0; k < UPR; ++k) {
