@@ -242,22 +242,29 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   constexpr uint32_t block_bytes = (uint32_t)T * 16;
   // DMA k of a chunk: lane l moves 16-byte unit j = l % 8 of block r = 8k + l / 8 of the group from
-  // swizzled slot j ^ (r / 2 % 8) (acs_persist.hpp viterbi_soft_persist). The offsets are recomputed
-  // from an opaque lane at every issue (8 VGPRs the ACS needs more).
+  // swizzled slot j ^ (r / 2 % 8) (acs_persist.hpp viterbi_soft_persist). r / 2 % 8 = l / 16 + 4 (k % 2)
+  // and a block is 768 B (bits 4-6 of r * 768 clear), so the lane's offset is one of two values,
+  // off_e (even k) and off_e ^ 64 (odd k), plus 8k blocks, a wave-uniform SGPR offset: the buffer
+  // form of the DMA then needs no VALU at all (the global form wanted a 64-bit VGPR address per DMA,
+  // recomputed from an opaque lane at every issue to save VGPRs the ACS needs).
+  static_assert(UPR == 8 && GRP == 2 && block_bytes % 128 == 0, "the two-offset form of the DMA swizzle");
+  const uint32_t off_e = (uint32_t)(lane / UPR) * block_bytes + (uint32_t)((lane % UPR) ^ (lane / 16)) * 16;
+  const uint32_t off_o = off_e ^ 64u;
   auto issue_chunk = [&](int g, int c, int buf) __attribute__((always_inline)) {
     int ln = threadIdx.x;
     asm volatile("" : "+v"(ln));
     if (g * kRegThreads + kRegThreads < nb) {
-      const unsigned char* base = in + (size_t)g * kRegThreads * block_bytes + c * PF * 16;
+      const __amdgpu_buffer_rsrc_t grp = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<unsigned char*>(in) + (size_t)g * kRegThreads * block_bytes, 0,
+          kRegThreads * block_bytes, 0x00020000);
 #pragma unroll
-      for (int k = 0; k < UPR; ++k) {
-        const int r = k * (kRegThreads / UPR) + ln / UPR, j = ln % UPR;
-        const uint32_t off = (uint32_t)r * block_bytes + (uint32_t)(j ^ ((r / GRP) % UPR)) * 16;
+      for (int k = 0; k < UPR; ++k)
         // nt (aux 2): the input is read once; 0.976x the time of the default policy (the decision
         // slots keep more of the caches, profiles/r03_k9_wide.txt); AB & 4: default policy
-        __builtin_amdgcn_global_load_lds(base + off, (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16), 16, 0,
-                                         (ABLATE & 4) ? 0 : 2);
-      }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(grp, (lds_ptr_t)(lds + buf * BUF + k * kRegThreads * 16), 16,
+                                                 (k & 1) ? off_o : off_e,
+                                                 c * PF * 16 + k * (kRegThreads / UPR) * (int)block_bytes, 0,
+                                                 (ABLATE & 4) ? 0 : 2);
     } else {
 #pragma unroll
       for (int k = 0; k < UPR; ++k) {
