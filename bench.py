@@ -337,6 +337,68 @@ def reduce_over_ranks(dist, wall, kernel_ms, errors, device):
     return float(t[0]), float(t[1]), [round(float(x.item()), 4) for x in per], int(e.item())
 
 
+def init_group(dist, torch, backend, world, device_index):
+    """The process group of this run. N > 1: the ranks torch.distributed.run started. N = 1 with an
+    explicit --backend: a world-size-1 group (127.0.0.1, a free port), so the exact collectives of an
+    N-GPU run -- the MAX / SUM all-reduces, the all-gather and the barriers, over RCCL on cuda with
+    nccl -- execute on a one-GPU box too. Returns the RCCL version string (nccl) or None."""
+    from ccviterbi import launch
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(launch.free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    dist.init_process_group("gloo")
+    return None
+
+
+def ber_curve(code, hard, frames, seed, rank, world, dist=None, device="cuda", noise=("f64",),
+              decode=None, frame_blocks=FRAME_BLOCKS, threads=None):
+    """The BER-vs-Eb/N0 half of the metric: the reference's sweep points (AWGN-channel/main.c:150-161:
+    Eb/N0 0..14 dB; BSC: binary-symmetric-channel/main.c:103-109), `frames` 1 M-bit frames per rank
+    per point, sharded as the sweep CLI shards them (contiguous frame ranges of each point's Philox
+    stream, sim.shard) and generated on the GPU (the on-device channel, sim.DeviceChannelDecoder) --
+    or decoded by `decode(info, data)` (tests: the oracle under gloo). One SUM all-reduce of the
+    [point][errors, bits] table and one MAX of the sweep time per noise mode. Returns
+    {mode: {"points": [...], "seconds", "gbit_s"}}."""
+    import torch
+    from ccviterbi import HARD, SOFT, channel as ch, sim
+    chan = HARD if hard else SOFT
+    points = list(ch.REFERENCE_P_PPM if hard else ch.REFERENCE_EBN0_DB)
+    bits_per_point = world * frames * frame_blocks * code.blen
+    curves = {}
+    for nz in (("bsc",) if hard else noise):
+        dev = None
+        if decode is None:
+            dev = sim.DeviceChannelDecoder(code, chan, frame_blocks, seed, noise_f32=nz == "f32",
+                                           chunk_blocks=frames * frame_blocks)
+            dev.warm_up(0.05, points[0])
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pts = sim.ber_sweep(code, points, chan, bits_per_point=lambda p: bits_per_point,
+                            frame_blocks=frame_blocks, seed=seed, rank=rank, world=world, decode=decode,
+                            reduce=False, device_decoder=dev, threads=threads)
+        secs = time.perf_counter() - t0
+        counters = np.array([[pt.errors, pt.bits] for pt in pts], np.int64)
+        if dist is not None:
+            counters = sim.all_reduce_counters(counters)
+            t = torch.tensor([secs], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            secs = float(t.item())
+        key = "p_ppm" if hard else "ebn0_db"
+        curves[nz] = {
+            "points": [{key: p, "errors": int(e), "bits": int(b), "ber": (int(e) / int(b)) if b else None}
+                       for p, (e, b) in zip(points, counters)],
+            "seconds": round(secs, 4),
+            "gbit_s": round(int(counters[:, 1].sum()) / secs / 1e9, 2) if secs > 0 else None,
+        }
+    return curves
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -376,7 +438,11 @@ def main(argv=None):
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="plan option (ccv_plan_set_option, include/ccv.h) for A/B runs; repeatable")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
-                    help="process-group backend for N > 1 (default nccl = RCCL over xGMI)")
+                    help="process-group backend for N > 1 (default nccl = RCCL over xGMI); given at N = 1 "
+                         "it forces a world-size-1 group, so the N-GPU collectives run on one GPU")
+    ap.add_argument("--curve-frames", type=int, default=None,
+                    help="1 M-bit frames per rank per point of the BER-vs-Eb/N0 curve run after the timed "
+                         "region (default: --frames, one launch per point); 0 = no curve")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on cuda:0, reductions over gloo")
     ap.add_argument("--no-hbm-probe", action="store_true",
@@ -406,11 +472,8 @@ def main(argv=None):
     device_index = 0 if args.same_device else local_rank
     backend = args.backend or ("gloo" if args.same_device else "nccl")
     torch.cuda.set_device(device_index)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
-        else:
-            dist.init_process_group("gloo")
+    use_pg = world > 1 or args.backend is not None
+    rccl_version = init_group(dist, torch, backend, world, device_index) if use_pg else None
 
     stack = args.decoder == "stack"
     sequential = args.decoder != "viterbi"
@@ -469,7 +532,7 @@ def main(argv=None):
     d_err.zero_()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -478,7 +541,7 @@ def main(argv=None):
         step()
         ends[k].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     wall = time.perf_counter() - t0
     step_ms = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
@@ -532,9 +595,17 @@ def main(argv=None):
                  "note": "same Philox frames generated on the GPU (encoder, mapper, Box-Muller AWGN, "
                          "demapper fused ahead of the ACS)"}
 
+    # the BER-vs-Eb/N0 half of the metric, after the timed region: every rank decodes its shard of
+    # each point's frames on the on-device channel, one all-reduce of the counters (RCCL over xGMI)
+    curve = None
+    curve_frames = args.frames if args.curve_frames is None else args.curve_frames
+    if curve_frames > 0 and not sequential:
+        curve = ber_curve(code, hard, curve_frames, args.seed, rank, world, dist if use_pg else None,
+                          "cuda" if backend == "nccl" else "cpu", noise=("f64", "f32"))
+
     errors = int(errs.item())
     per_rank_kernel_ms = [round(kernel_ms, 4)]
-    if world > 1:   # MAX of the timings, SUM of the error counters (RCCL over xGMI)
+    if use_pg:   # MAX of the timings, SUM of the error counters (RCCL over xGMI)
         wall, kernel_ms, per_rank_kernel_ms, errors = reduce_over_ranks(
             dist, wall, kernel_ms, errors, "cuda" if backend == "nccl" else "cpu")
     bits_per_step = world * nb * code.blen
@@ -613,7 +684,8 @@ def main(argv=None):
                 "channel": args.channel,
                 **({"p_ppm": args.p_ppm} if hard else {"ebn0_db": args.ebn0}),
                 "parallelism": f"dp{world} (frames sharded, counters all-reduced once)",
-                "backend": backend if world > 1 else None,
+                "backend": backend if use_pg else None,
+                "rccl_version": rccl_version,
                 "same_device_rehearsal": bool(args.same_device),
                 "kernel": plan.kernel,
                 "variant": getattr(plan, "variant", plan.kernel),
@@ -664,9 +736,12 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "cpu_baseline_optimized": cpu_opt,
             "fused_channel": fused,
+            "ber_curve": ({"frames_per_gpu_per_point": curve_frames, "data": "on-device channel "
+                           "(Philox, the reference's noise scaling), stream of point k = (seed, k << 40 | block)",
+                           **curve} if curve else None),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

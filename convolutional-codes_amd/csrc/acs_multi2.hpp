@@ -224,7 +224,7 @@ constexpr int kMulti2StepOff(int step, int stepb) { return CCV_MULTI2_SLOT_ABLAT
 #ifndef CCV_MULTI2_WAVES
 #define CCV_MULTI2_WAVES 2
 #endif
-template <CodeSpec C, int BLEN, int LB = 7>
+template <CodeSpec C, int BLEN, int LB = 7, int OPT = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(CCV_MULTI2_WAVES)))
 void viterbi_multi2_slot(RegArgs a, int ngroups) {
   using X = Multi2<C, LB>;
@@ -249,7 +249,6 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
   const int q = lane & 1;
   const bool qb = q != 0;
   const int nb = a.nblocks;
-  const int stride_groups = gridDim.x;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * BUF];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);
   // DMA k of a chunk: unit k*64 + lane = block r (of 32), LDS slot j of its row, holding step
@@ -278,11 +277,12 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
   constexpr int kSc1 = 16;   // cache policy: agent scope (sc1), the load misses the CU's L1
 
   uint32_t errors = 0;
-  int g = blockIdx.x;
+  GroupWalk<OPT> walk(a, ngroups, lane, queue_hops(OPT));
+  int g = walk.first();
   if (g < ngroups) issue_chunk(g, 0, 0);
-  for (; g < ngroups; g += stride_groups) {
+  walk.started(g);
+  for (int nxt = 0; g < ngroups; g = nxt) {
     const int blk = g * BPG + rblk;
-    const bool has_next = g + stride_groups < ngroups;
     float M[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) M[r] = (q == 0 && r == 0) ? 0.0f : __builtin_inff();
@@ -299,8 +299,13 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
         asm volatile("" ::: "memory");   // info loads before the DMA (vmcnt order)
       }
       const int buf = p & 1;
-      if (p + 1 < NPER) issue_chunk(g, p + 1, buf ^ 1);
-      else issue_chunk(has_next ? g + stride_groups : g, 0, buf ^ 1);
+      if (p + 1 < NPER) {
+        issue_chunk(g, p + 1, buf ^ 1);
+      } else {   // the next group's first chunk (a harmless reload of this one's when there is none)
+        nxt = walk.next(g);
+        issue_chunk(nxt < ngroups ? nxt : g, 0, buf ^ 1);
+        walk.issued(nxt);
+      }
       const uint32_t rd = row + (uint32_t)(buf * BUF);
       f32x4 rowv = lds_read_b128<0>(rd + swz);
       auto phase_at = [&]<int P>() __attribute__((always_inline)) {
@@ -415,6 +420,7 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     }
   }
   wait_vmcnt<0>();   // the look-ahead DMA writes LDS: it must land before the workgroup ends
+  walk.done();
   accumulate_errors(a, errors);
 }
 

@@ -190,6 +190,149 @@ __device__ __forceinline__ uint64_t load_info(const RegArgs& a, int b) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Group schedule. Round 1-5 kernels walked g, g + grid, ... (a static share per wave). The waves of a
+// SIMD do not progress alike: VALU issue is arbitrated by age, so the oldest wave runs nearly
+// unimpeded and the youngest gets the leftover slots; with equal static shares the youngest sets the
+// kernel length (round-5 PMC: waves resident 0.87 of the headline kernel's cycles, 0.69 of the BSC
+// K = 7 kernel's at 3 waves per SIMD). With the queue (kPersistQueue) every wave starts on one static
+// group and then takes the next free group: a wave that progresses faster simply decodes more groups.
+//
+// One head per XCD label (blockIdx.x % 8: the workgroups of a label share an XCD under the
+// round-robin placement; speed only, never correctness) over a contiguous eighth of the groups, on
+// 128-byte lines of their own: 40,625 groups per 0.5 ms would be ~81 dequeues/us on one word, at its
+// measured ceiling (~88/us, MI355X_MICROARCH.md "dequeue"); eight heads take ~10/us each. A label whose
+// range is exhausted steals from the next labels in turn. Tickets are agent-scope atomics (performed
+// at the memory side, coherent across XCDs) from lane 0, fetched one group AHEAD so their latency
+// (~1-3 us) hides behind a whole group's work; only the steals at the very end are synchronous.
+// The queue is self-resetting: every wave adds 1 to the exit word after its last ticket, and the wave
+// that adds last (it has seen grid - 1) zeroes the heads and the exit word, so the next launch on the
+// stream starts from zeros (graph replays included). A plan's launches are stream-ordered, as for
+// its other scratch.
+constexpr int kQueueLabels = 8;
+constexpr int kQueueStride = 32;                                  // u32 words per head: 128 B
+constexpr int kQueueWords = (kQueueLabels + 1) * kQueueStride;   // heads + the exit word
+constexpr int kStampWords = 8;                                    // diagnostic stamps per wave
+
+struct GroupQueue {
+  uint32_t* q;
+  int ngroups, grid, label;
+  __device__ __forceinline__ int lo(int x) const {
+    return (int)((long long)x * ngroups / kQueueLabels);
+  }
+  // statically assigned groups of label x: its waves' first groups (blocks x, x + 8, ...)
+  __device__ __forceinline__ int nstatic(int x) const {
+    const int waves = grid > x ? (grid - x + kQueueLabels - 1) / kQueueLabels : 0;
+    const int range = lo(x + 1) - lo(x);
+    return waves < range ? waves : range;
+  }
+  // ticket from head x: lane 0 draws it, the caller reads it with read_lane(t, 0). The address carries
+  // an opaque zero VGPR: on a uniform address the compiler's atomic optimizer rewrites the fetch into
+  // its per-lane form (mbcnt + readfirstlane of the result), which waits for the atomic right there.
+  // (A snapshot of the other heads in the same instruction -- lanes 1..7 adding 0 -- multiplies the
+  // atomic traffic per head by 8, past one word's ~88/us ceiling: 1.27-1.46x the static walk's time,
+  // profiles/r06b.)
+  __device__ __forceinline__ uint32_t fetch(int x, int lane) const {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    uint32_t t = 0;
+    if (lane == 0)
+      t = __hip_atomic_fetch_add(q + x * kQueueStride + z, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t;
+  }
+  // ticket t of head qx -> group (wave-uniform). Every label's own waves drain its head (the queue is
+  // only used with a wave on every label, grid >= 8); an exhausted head sends the wave to the next
+  // label's head for at most `hops` synchronous tickets (balancing between XCDs, the tail only).
+  // ngroups when done. `syncs` counts the synchronous tickets.
+  __device__ __forceinline__ int resolve(uint32_t t, int& qx, int lane, uint32_t& syncs, int hops) const {
+    int grp = lo(qx) + nstatic(qx) + (int)read_lane(t, 0);
+    while (grp >= lo(qx + 1)) {
+      if ((qx - label + kQueueLabels) % kQueueLabels >= hops) return ngroups;
+      qx = (qx + 1) % kQueueLabels;
+      ++syncs;
+      grp = lo(qx) + nstatic(qx) + (int)read_lane(fetch(qx, lane), 0);
+    }
+    return grp;
+  }
+  __device__ __forceinline__ int first(int lane, int& qx, uint32_t& syncs, int hops) const {
+    const int j = blockIdx.x / kQueueLabels;
+    if (j < lo(label + 1) - lo(label)) return lo(label) + j;
+    return resolve(fetch(qx, lane), qx, lane, syncs, hops);
+  }
+  // lane i of a fetch as a wave-uniform value. Inline asm: the builtin readfirstlane of a loop-carried
+  // ticket is pushed into the predecessors by the compiler, i.e. right behind the fetch, with a
+  // vmcnt(0) wait for the atomic there -- the latency the look-ahead exists to hide.
+  __device__ __forceinline__ static uint32_t read_lane(uint32_t t, int i) {
+    uint32_t r;
+    asm volatile("v_readlane_b32 %0, %1, %2" : "=s"(r) : "v"(t), "s"(i));
+    return r;
+  }
+  // after the wave's last ticket: the last wave out zeroes the queue for the next launch
+  __device__ __forceinline__ void exit(int lane) const {
+    if (lane == 0) {
+      uint32_t* done = q + kQueueLabels * kQueueStride;
+      const uint32_t d = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (uint32_t)grid - 1) {
+#pragma unroll
+        for (int x = 0; x <= kQueueLabels; ++x)
+          __hip_atomic_exchange(q + x * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+};
+
+// The group walk of a persistent kernel as one object (the K = 9 kernels, acs_wide.hpp /
+// acs_multi2.hpp): static (g, g + grid, ...) or, with OPT & kPersistQueue, the queue. first() before
+// the first group's DMA, started() after it; next(g) where the next group's first DMA is issued (the
+// queue resolves the ticket fetched a group ago), issued(nxt) right after that DMA; done() at exit.
+template <int OPT>
+struct GroupWalk {
+  static constexpr bool QUEUE = (OPT & 1024) != 0;   // kPersistQueue (declared below)
+  GroupQueue Q;
+  int lane, qx, hops;
+  uint32_t syncs = 0, ticket = 0;
+  __device__ __forceinline__ GroupWalk(const RegArgs& a, int ngroups, int lane_, int max_hops)
+      : Q{a.queue, ngroups, (int)gridDim.x, (int)(blockIdx.x % kQueueLabels)}, lane(lane_), qx(Q.label),
+        hops((int)gridDim.x < kQueueLabels ? kQueueLabels - 1 : max_hops) {}
+  __device__ __forceinline__ int first() { return QUEUE ? Q.first(lane, qx, syncs, hops) : (int)blockIdx.x; }
+  __device__ __forceinline__ void started(int g) {
+    if (QUEUE && g < Q.ngroups) ticket = Q.fetch(qx, lane);
+  }
+  __device__ __forceinline__ int next(int g) {
+    return QUEUE ? Q.resolve(ticket, qx, lane, syncs, hops) : g + (int)gridDim.x;
+  }
+  __device__ __forceinline__ void issued(int nxt) {
+    if (QUEUE && nxt < Q.ngroups) ticket = Q.fetch(qx, lane);
+  }
+  __device__ __forceinline__ void done() {
+    if constexpr (QUEUE) Q.exit(lane);
+  }
+};
+
+// Diagnostic stamps (kPersistStamp builds only; production never stamps): per wave, lane 0 writes
+// {start lo, start hi, end lo, end hi (s_memrealtime, 100 MHz), HW_ID, XCC_ID, groups decoded, steals}
+// with vector stores to a buffer of their own (tools/persist_bench.hip "tail").
+__device__ __forceinline__ uint32_t hw_id_reg() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t xcc_id_reg() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v;
+}
+__device__ __forceinline__ void write_stamps(uint32_t* stamps, int lane, uint64_t t0, uint32_t groups,
+                                             uint32_t steals) {
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) {
+    uint4* p = reinterpret_cast<uint4*>(stamps + (size_t)blockIdx.x * kStampWords);
+    p[0] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+    p[1] = make_uint4(hw_id_reg(), xcc_id_reg(), groups, steals);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Soft decision, r = 1/2 (16-byte steps), block-major input [nb][T][4] staged by LDS-DMA in 8-step
 // (128-byte) chunks per block, XOR-swizzled rows as in viterbi_soft_reg, one chunk in flight: the DMA
 // of chunk c+1 (of this group, or chunk 0 of the next) is issued as soon as chunk c has been read
@@ -224,7 +367,18 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 // ds_write instead of LDS-DMA (1.5 % slower).
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
              kPersistDepth2 = 16, kPersistNoMemRandom = 64, kPersistNoDma = 128, kPersistNoLdsRead = 256,
-             kPersistInputNt = 512 };
+             kPersistInputNt = 512, kPersistQueue = 1024, kPersistStamp = 2048,
+             kPersistInfoFirst = 4096, kPersistQueueHop1 = 8192, kPersistQueueHop7 = 16384 };
+// Production schedules (round 6, tools/tail_bench.hip, profiles/r06c): the group queue with full
+// stealing -- soft 0.982x the static walk's time, hard 0.869x (+ the info loads ahead of the DMA, 0.997x
+// alone); 0, 1 or 7 steal hops measured alike.
+constexpr int kPersistSoftProd = kPersistQueue | kPersistQueueHop7;
+constexpr int kPersistHardProd = kPersistQueue | kPersistQueueHop7 | kPersistInfoFirst;
+static_assert(kPersistQueue == 1024, "GroupWalk::QUEUE");
+// steal hops of the queue schedule (GroupQueue::resolve): 0, or the OPT bits above
+constexpr int queue_hops(int opt) {
+  return (opt & kPersistQueueHop7) ? kQueueLabels - 1 : (opt & kPersistQueueHop1) ? 1 : 0;
+}
 
 template <CodeSpec C, int BLEN, int ABLATE = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
@@ -298,14 +452,27 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
                            (uint32_t)(((lane / GRP) % UPR) * 16);
 
   uint32_t errors = 0;
-  int g = blockIdx.x;
+  constexpr bool QUEUE = (ABLATE & kPersistQueue) != 0, STAMP = (ABLATE & kPersistStamp) != 0;
+  constexpr int HOPS = queue_hops(ABLATE);
+  static_assert(!(QUEUE && DEPTH2), "the queue resolves one group ahead");
+  static_assert(!(QUEUE && (ABLATE & kPersistNoMem)), "the next group is resolved with the DMA");
+  const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
+  if constexpr (STAMP) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const GroupQueue Q{a.queue, ngroups, (int)gridDim.x, (int)(blockIdx.x % kQueueLabels)};
+  int qx = Q.label;
+  uint32_t steals = 0, ndone = 0, ticket = 0;
+  // fewer waves than labels (a batch of < 8 groups): every head must be reachable
+  const int hops = (int)gridDim.x < kQueueLabels ? kQueueLabels - 1 : HOPS;
+  int g = QUEUE ? Q.first(lane, qx, steals, hops) : (int)blockIdx.x;
   if (!(ABLATE & kPersistNoMem) && g < ngroups) {
     issue_chunk(g, 0, 0);
     if constexpr (DEPTH2) issue_chunk(g, 1, 1);
   }
-  for (; g < ngroups; g += stride_groups) {
+  if (QUEUE && g < ngroups) ticket = Q.fetch(qx, lane);
+  for (int nxt = 0; g < ngroups; g = QUEUE ? nxt : g + stride_groups) {
     const int b = g * kRegThreads + lane;
     const bool has_next = g + stride_groups < ngroups;
+    ++ndone;
     float M[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) M[s] = s ? __builtin_inff() : 0.0f;   // viterbi-decoder.c:212-218
@@ -358,8 +525,17 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
           asm volatile("" ::: "memory");   // keep the info loads before the DMA (issue order above)
         }
         if constexpr (!DEPTH2) {
-          if constexpr (c + 1 < NCH) issue_chunk(g, c + 1, 0);
-          else issue_chunk(has_next ? g + stride_groups : g, 0, 0);
+          if constexpr (c + 1 < NCH) {
+            issue_chunk(g, c + 1, 0);
+          } else if constexpr (QUEUE) {
+            // the next group from the ticket fetched a group ago, its first chunk's DMA, then the
+            // ticket of the group after it (returns long before it is read, at that group's last chunk)
+            nxt = Q.resolve(ticket, qx, lane, steals, hops);
+            issue_chunk(nxt < ngroups ? nxt : g, 0, 0);
+            if (nxt < ngroups) ticket = Q.fetch(qx, lane);
+          } else {
+            issue_chunk(has_next ? g + stride_groups : g, 0, 0);
+          }
         } else if constexpr (c + 2 < NCH) {
           issue_chunk(g, c + 2, c % 2);
         } else {
@@ -414,7 +590,9 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   // the last group's look-ahead DMAs write LDS: they must land before the workgroup (and its LDS
   // allocation) ends
   wait_vmcnt<0>();
+  if constexpr (QUEUE) Q.exit(lane);
   accumulate_errors(a, errors);
+  if constexpr (STAMP) write_stamps(a.stamps, lane, t_start, ndone, steals);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -443,7 +621,7 @@ __device__ __forceinline__ uint32_t lds_read_u8(uint32_t addr) {
 // 104-frame launch, 239 instead of 225 Gbit/s (profiles/r05c/ab/bsc2_*). Also measured in round 5
 // (profiles/r05a/ab/bsc_*, u16): no scheduling barrier between steps, the next chunk's symbols read a
 // chunk ahead, two popcounts for the four branch metrics -- all within +-0.8 %.
-template <CodeSpec C, int BLEN, int MMODE = 3>
+template <CodeSpec C, int BLEN, int MMODE = 3, int OPT = 0>
 __global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
 void viterbi_hard_persist(RegArgs a, int ngroups) {
   constexpr int S = 1 << (C.K - 1);
@@ -487,17 +665,46 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
   };
 
   uint32_t errors = 0;
-  int g = blockIdx.x;
+  // group schedule (see GroupQueue): OPT & kPersistQueue takes groups from the queue, kPersistStamp
+  // writes the diagnostic stamps
+  constexpr bool QUEUE = (OPT & kPersistQueue) != 0, STAMP = (OPT & kPersistStamp) != 0;
+  constexpr int HOPS = queue_hops(OPT);
+  const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
+  if constexpr (STAMP) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const GroupQueue Q{a.queue, ngroups, (int)gridDim.x, (int)(blockIdx.x % kQueueLabels)};
+  int qx = Q.label;
+  uint32_t steals = 0, ndone = 0, ticket = 0;
+  // fewer waves than labels (a batch of < 8 groups): every head must be reachable
+  const int hops = (int)gridDim.x < kQueueLabels ? kQueueLabels - 1 : HOPS;
+  int g = QUEUE ? Q.first(lane, qx, steals, hops) : (int)blockIdx.x;
   int buf = 0;
   if (g < ngroups) issue_group(g, 0);
-  for (; g < ngroups; g += stride_groups, buf ^= 1) {
+  if (QUEUE && g < ngroups) ticket = Q.fetch(qx, lane);
+  for (int nxt = 0; g < ngroups; g = QUEUE ? nxt : g + stride_groups, buf ^= 1) {
     const int b = g * kRegThreads + lane;
+    ++ndone;
     // this group's bytes must have landed before the first read (vmcnt also covers the previous
-    // group's output stores, long retired by now)
+    // group's output stores, long retired by now, and the queue ticket fetched a group ago)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (g + stride_groups < ngroups) issue_group(g + stride_groups, buf ^ 1);
+    // kPersistInfoFirst: the info loads ahead of the next group's DMA, so that their wait (at the
+    // error count) is a counted vmcnt; behind it, as in rounds 2-5, the compiler waits vmcnt(0) for
+    // them right here -- i.e. for the next group's DMA (and the queue ticket) at every group start
+    uint64_t info = 0;
+    if constexpr ((OPT & kPersistInfoFirst) != 0) {
+      info = load_info<BLEN>(a, b);
+      asm volatile("" ::: "memory");
+    }
+    if constexpr (QUEUE) {
+      nxt = Q.resolve(ticket, qx, lane, steals, hops);
+      if (nxt < ngroups) {
+        issue_group(nxt, buf ^ 1);
+        ticket = Q.fetch(qx, lane);
+      }
+    } else if (g + stride_groups < ngroups) {
+      issue_group(g + stride_groups, buf ^ 1);
+    }
     const uint32_t row_addr = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * kBuf + lane * T);
-    const uint64_t info = load_info<BLEN>(a, b);
+    if constexpr ((OPT & kPersistInfoFirst) == 0) info = load_info<BLEN>(a, b);
     // metric type (see above): 3 = fp32 (production); 2 = plain uint16_t (v_add_u16 / v_min_u16,
     // rounds 2-4); 0 = H16 inline-asm ops (round 2 first cut: hipcc puts an s_nop 0 after every
     // inline-asm VALU whose result is read next, 6 % slower than 2); 1 = u32 (v_bcnt-folded adds and
@@ -575,7 +782,9 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
     const uint64_t bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
     errors += emit_block<T, BLEN>(a, b, bits, info);
   }
+  if constexpr (QUEUE) Q.exit(lane);
   accumulate_errors(a, errors);
+  if constexpr (STAMP) write_stamps(a.stamps, lane, t_start, ndone, steals);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -261,6 +261,8 @@ struct RegArgs {
   void* dec;               // [T][dec_stride] DecWord
   const uint8_t* info;     // optional [nb][IB] transmitted info bytes (error counting)
   unsigned long long* err; // optional error accumulator
+  uint32_t* queue;         // persistent kernels: the group queue (acs_persist.hpp GroupQueue), zeroed
+  uint32_t* stamps;        // diagnostic builds only (kPersistStamp): 8 words per wave
 };
 
 constexpr int kRegThreads = 64;   // one wave per workgroup: spreads small batches over more CUs

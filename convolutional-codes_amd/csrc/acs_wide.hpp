@@ -232,7 +232,6 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   static_assert(T <= 64, "the history fits 64 bits");
   const int lane = threadIdx.x;
   const int nb = a.nblocks;
-  const int stride_groups = gridDim.x;
 
   // two chunk buffers: chunk c lives in buffer c % 2 (NCH is even, so the parity carries across
   // groups), and the DMA of chunk c + 1 may start as soon as chunk c's rows are due -- the rows are
@@ -296,11 +295,12 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
   }
 
   uint32_t errors = 0;
-  int g = blockIdx.x;
+  GroupWalk<ABLATE> walk(a, ngroups, lane, queue_hops(ABLATE));
+  int g = walk.first();
   if (g < ngroups) issue_chunk(g, 0, 0);
-  for (; g < ngroups; g += stride_groups) {
+  walk.started(g);
+  for (int nxt = 0; g < ngroups; g = nxt) {
     const int b = g * kRegThreads + lane;
-    const bool has_next = g + stride_groups < ngroups;
     float M[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) M[s] = s ? __builtin_inff() : 0.0f;   // viterbi-decoder.c:212-218
@@ -316,8 +316,13 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
       if ((ABLATE & 1) == 0 && c >= 2) wait_vmcnt<16>();
       else wait_vmcnt<0>();
       const int buf = c & 1;
-      if (c + 1 < NCH) issue_chunk(g, c + 1, buf ^ 1);
-      else issue_chunk(has_next ? g + stride_groups : g, 0, buf ^ 1);
+      if (c + 1 < NCH) {
+        issue_chunk(g, c + 1, buf ^ 1);
+      } else {   // the next group's first chunk (a harmless reload of this one's when there is none)
+        nxt = walk.next(g);
+        issue_chunk(nxt < ngroups ? nxt : g, 0, buf ^ 1);
+        walk.issued(nxt);
+      }
       const uint32_t rd = rd_base + (uint32_t)(buf * BUF);
       f32x4 row = lds_read_b128<0>(rd);
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
@@ -455,6 +460,7 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
     }
   }
   wait_vmcnt<0>();   // the look-ahead DMA writes LDS: it must land before the workgroup ends
+  walk.done();
   accumulate_errors(a, errors);
 }
 

@@ -136,6 +136,7 @@ struct ccv_plan {
   DeviceBuffer sim_info, sim_out;             // ccv_simulate_device scratch (caller passed none)
   DeviceBuffer sim_frames;                    // ccv_simulate_device: K = 9 frames ahead of the wide decode
   DeviceBuffer hard_rows;                     // K = 9 BSC: the symbols as Hamming-distance rows (hard_rows)
+  DeviceBuffer queue;                         // persistent kernels' group queue (acs_persist.hpp GroupQueue)
   hipStream_t stream = nullptr;      // plan-owned stream for ccv_decode_host
   // ccv_plan_set_option (include/ccv.h): kernel A/B switches per plan; defaults = production paths
   struct Options {
@@ -488,6 +489,15 @@ int ccv_plan_create(ccv_plan** out, int channel, int n, int K, int blen, const u
     delete p;
     return fail("hipStreamCreate failed");
   }
+  // the persistent kernels' group queue: zeroed once here, then reset by each launch's last wave
+  if (register_path(*p) &&
+      (p->queue.grow(ccv::kQueueWords * sizeof(uint32_t), p->stream) ||
+       hipMemset(p->queue.ptr, 0, ccv::kQueueWords * sizeof(uint32_t)) != hipSuccess)) {
+    (void)hipGetLastError();
+    const std::string why = g_last_error;
+    ccv_plan_destroy(p);
+    return fail("group queue allocation failed: %s", why.c_str());
+  }
   *out = p;
   return 0;
 }
@@ -548,6 +558,7 @@ void ccv_plan_destroy(ccv_plan* p) {
   p->sim_out.release();
   p->sim_frames.release();
   p->hard_rows.release();
+  p->queue.release();
   p->counter.release();
   p->symtab.release();
   p->order.release();
@@ -622,7 +633,13 @@ int ccv_plan_persistent_waves(const ccv_plan* p, int fresh) {
 
 int ccv_plan_reserve(ccv_plan* p, size_t max_blocks) {
   if (!p) return fail("null plan");
-  if (const ccv::RegLaunchFn wide = wide_kernel(*p, false)) return grow_wide_scratch(*p, wide, p->stream);
+  if (const ccv::RegLaunchFn wide = wide_kernel(*p, false)) {
+    if (grow_wide_scratch(*p, wide, p->stream)) return -1;
+    // BSC: the Hamming-distance rows ccv_decode_device builds ahead of the soft kernel (16 B per step)
+    if (p->d.channel == CCV_HARD)
+      return p->hard_rows.grow(max_blocks * (size_t)p->d.steps * sizeof(float4), p->stream);
+    return 0;
+  }
   if (persist_kernel(*p, false)) {
     // hard: a partial last group of < 64 blocks runs on viterbi_hard_reg with HBM decisions
     if (p->d.channel != CCV_HARD) return 0;
@@ -664,6 +681,7 @@ int ccv_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_t* d_
     a.path_metric = hard ? d_path_metric : nullptr;
     a.info = d_info;
     a.err = d_info ? d_errors : nullptr;
+    a.queue = static_cast<uint32_t*>(p->queue.ptr);
     if (const ccv::RegLaunchFn wide = wide_kernel(*p, d_decisions != nullptr)) {
       // decisions in a per-wave scratch slot, groups of 64 (one lane per block, acs_wide.hpp) or 16
       // (four lanes per block, acs_multi.hpp viterbi_multi_slot) blocks
