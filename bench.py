@@ -261,10 +261,13 @@ def valu_fraction(pmc):
 # PMC byte scales (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of a wide
 # coalesced read on gfx950, WRITE_SIZE the exact bytes of 16-byte-per-lane stores.
 PMC_FETCH_SCALE, PMC_WRITE_SCALE = 2.0, 1.0
-PMC_SCALE_NOTE = ("FETCH_SIZE x 2, WRITE_SIZE x 1 as the guide prescribes for gfx950. The in-run device "
-                  "copy calibration (pmc_calibration) can read a higher read scale (2.67 in some runs), "
-                  "but that scale would put the decode's traffic above the measured achievable HBM rate "
-                  "(hbm_read_gbs), which is impossible; x 2 is the consistent reading.")
+def pmc_scale_note(cal):
+    """How the PMC byte scales were chosen, with the in-run calibration they are checked against."""
+    if not cal or "read_scale" not in cal:
+        return "FETCH_SIZE x 2, WRITE_SIZE x 1 as the guide prescribes for gfx950 (no in-run calibration copy)"
+    return (f"FETCH_SIZE x 2, WRITE_SIZE x 1 as the guide prescribes for gfx950; the PMC run's own device copy "
+            f"of {cal['copy_bytes']} B (largest-grid copy dispatches, tools/pmc_workload.py calibration) reads "
+            f"{cal['read_scale']:.3f} / {cal['write_scale']:.3f}")
 
 
 HBM_PROBE_MIN_BYTES = 104 * 25000 * 46 * 16   # the headline's input batch, 1.91 GB
@@ -730,7 +733,7 @@ def main(argv=None):
                 **hbm_ceiling_fields(hbm_probe, traffic, kernel_ms),
                 "pmc_scale_used": {"fetch": PMC_FETCH_SCALE, "write": PMC_WRITE_SCALE} if traffic else None,
                 "pmc_calibration": pmc.get("calibration") if traffic else None,
-                "pmc_scale_note": PMC_SCALE_NOTE if traffic else None,
+                "pmc_scale_note": pmc_scale_note(pmc.get("calibration")) if traffic else None,
                 "bound_basis": bound_basis,
             },
             "cpu_baseline": cpu,

@@ -44,3 +44,36 @@ def test_hbm_ceiling_fields():
     assert abs(f["traffic_frac_of_achievable"] - 2.625e9 / 0.5e-3 / 1e9 / 7000.0) < 1e-4
     assert bench.HBM_PROBE_MIN_BYTES == 104 * 25000 * 46 * 16
     assert 0 < bench.LATENCY_BOUND_BELOW < 0.5
+
+
+def test_pmc_calibration_uses_the_largest_copy_only(tmp_path):
+    """The calibration copy's FETCH_SIZE / WRITE_SIZE scales come from the copy kernel's largest-grid
+    dispatches only: a run also holds a 512-thread 1.6 KiB copy of the same kernel, and averaging it in
+    read 2.67 / 1.33 instead of 2.00 / 1.00 (VERDICT r05 weak #7). Rows as rocprofv3 writes them."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import pmc_workload as P
+    head = ('"Correlation_Id","Dispatch_Id","Agent_Id","Queue_Id","Process_Id","Thread_Id","Grid_Size",'
+            '"Kernel_Id","Kernel_Name","Workgroup_Size","LDS_Block_Size","Scratch_Size","VGPR_Count",'
+            '"Accum_VGPR_Count","SGPR_Count","Counter_Name","Counter_Value","Start_Timestamp","End_Timestamp"\n')
+    copy_bytes = 1913600000
+
+    def row(d, grid, kernel, counter, value):
+        return f'{d},{d},"Agent 2",1,7,7,{grid},7,"{kernel}",512,0,0,8,0,32,"{counter}",{value},1,2\n'
+    fetch = tmp_path / "f.csv"
+    write = tmp_path / "w.csv"
+    big_f = copy_bytes / 2 / 1024   # FETCH_SIZE counts half the bytes of a wide streaming read
+    fetch.write_text(head + "".join(row(d, 131072, "__amd_rocclr_copyBuffer", "FETCH_SIZE", big_f) for d in (1, 2, 3))
+                     + row(5, 512, "__amd_rocclr_copyBuffer", "FETCH_SIZE", 1.625)
+                     + row(6, 2048, "ccv::viterbi_soft_persist", "FETCH_SIZE", 1.0e6))
+    write.write_text(head + "".join(row(d, 131072, "__amd_rocclr_copyBuffer", "WRITE_SIZE", copy_bytes / 1024)
+                                    for d in (1, 2, 3))
+                     + row(5, 512, "__amd_rocclr_copyBuffer", "WRITE_SIZE", 1.625))
+    cal = P.calibration(P.counter_rows([str(fetch)]), P.counter_rows([str(write)]), copy_bytes)
+    assert abs(cal["read_scale"] - 2.0) < 1e-9 and abs(cal["write_scale"] - 1.0) < 1e-9
+    assert cal["copies_averaged"] == [3, 3]
+    # the committed records carry the rule's figures
+    doc = json.load(open(os.path.join(REPO, "profiles", "pmc_workloads.json")))
+    for key, rec in doc.items():
+        c = rec.get("calibration") or {}
+        if "copies_averaged" in c:
+            assert abs(c["read_scale"] - 2.0) < 0.01 and abs(c["write_scale"] - 1.0) < 0.001, key
