@@ -443,6 +443,11 @@ def main(argv=None):
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
                     help="process-group backend for N > 1 (default nccl = RCCL over xGMI); given at N = 1 "
                          "it forces a world-size-1 group, so the N-GPU collectives run on one GPU")
+    ap.add_argument("--step-events", choices=("on", "off"), default="off",
+                    help="off (default): one HIP event pair around the K timed steps on the decode stream "
+                         "(kernel_ms = its time / K, the ~1 us launch gaps included); on: a pair around "
+                         "every step as in rounds 1-5 -- the event records cost ~5 us per step "
+                         "(profiles/r06_events: 208.6 vs 210.3 Gbit/s)")
     ap.add_argument("--curve-frames", type=int, default=None,
                     help="1 M-bit frames per rank per point of the BER-vs-Eb/N0 curve run after the timed "
                          "region (default: --frames, one launch per point); 0 = no curve")
@@ -535,21 +540,31 @@ def main(argv=None):
     d_err.zero_()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_all = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev_all[0].record(stream)
     for k in range(args.steps):
-        starts[k].record(stream)
+        if args.step_events == "on":
+            starts[k].record(stream)
         step()
-        ends[k].record(stream)
+        if args.step_events == "on":
+            ends[k].record(stream)
+    ev_all[1].record(stream)
     torch.cuda.synchronize()
     if use_pg:
         dist.barrier()
     wall = time.perf_counter() - t0
-    step_ms = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
-    kernel_ms = sum(step_ms) / args.steps
-    kernel_ms_median = step_ms[len(step_ms) // 2]
+    steps_ms = ev_all[0].elapsed_time(ev_all[1])   # device time of the K timed steps, gaps included
+    if args.step_events == "on":
+        step_ms = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
+        kernel_ms = sum(step_ms) / args.steps
+        kernel_ms_median = step_ms[len(step_ms) // 2]
+    else:
+        kernel_ms = steps_ms / args.steps
+        kernel_ms_median = None
 
     errs = d_err.clone()   # the timed steps' error count (the informational runs below add more)
 
@@ -623,6 +638,13 @@ def main(argv=None):
         # as HBM bytes here; the PMC traffic says what actually crossed)
         on_chip = sequential or getattr(plan, "decisions", "hbm") in ("registers", "lds")
         hbm_bpb = algorithmic_bytes_per_bit(code, soft=not hard, decisions=not on_chip)
+        # K = 8 / 9 BSC on the soft persistent kernels: ccv_decode_device first turns each 1-byte symbol
+        # into a 16-byte Hamming-distance row (core.hip hard_rows, inside the timed step), which the
+        # decode then reads instead of the byte: +16 B written and +16 B read per step cross HBM
+        conv_bpb = 0.0
+        if hard and not sequential and getattr(plan, "variant", "") in ("persistent-wide", "persistent-slot2"):
+            conv_bpb = code.steps * 32.0 / code.blen
+            hbm_bpb += conv_bpb
         bytes_per_launch = bpb * nb * code.blen
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         hbm_achieved = hbm_bpb * nb * code.blen / (kernel_ms * 1e-3) / 1e9
@@ -637,6 +659,10 @@ def main(argv=None):
             bound_basis = ("the larger of traffic_frac (PMC HBM bytes / kernel time / 8 TB/s) and "
                            "valu_frac (SQ_INSTS_VALU / (512 per cycle x GRBM_GUI_ACTIVE / 8)); "
                            "frac / achieved / peak stay the SURVEY 8(d) HBM figure")
+            if conv_bpb:
+                bound_basis += ("; kernel_ms spans the Hamming-row conversion AND the decode, while the PMC "
+                                "record (traffic, valu_frac) is the decode kernel's alone: both fractions "
+                                "are lower bounds here, the conversion's 32 B per step are in hbm_bytes_per_bit")
             if max(valu_frac, traffic_frac) < LATENCY_BOUND_BELOW:
                 # neither pipe is near busy: the waves' dependent chains (and, for the sequential
                 # decoders, lanes idle behind the longest searches) set the time
@@ -702,7 +728,8 @@ def main(argv=None):
                     "errors": errors, "bits": bits_per_step * args.steps,
                     "ber": errors / (bits_per_step * args.steps)},
             "kernel_ms": round(kernel_ms, 4),
-            "kernel_ms_median": round(kernel_ms_median, 4),
+            "kernel_ms_median": round(kernel_ms_median, 4) if kernel_ms_median is not None else None,
+            "timed_steps_device_ms": round(steps_ms, 4),
             "per_rank_kernel_ms": per_rank_kernel_ms,
             "clock_warmup_s": args.clock_warmup,
             # per rank, before the timed region: the host producer (Philox channel on cpu_threads()
@@ -722,6 +749,7 @@ def main(argv=None):
                 "algorithmic_bytes_per_bit": round(bpb, 4),
                 "bytes_per_launch": int(bytes_per_launch),
                 "hbm_bytes_per_bit": round(hbm_bpb, 4),
+                "conversion_bytes_per_bit": round(conv_bpb, 4) if conv_bpb else None,
                 "hbm_achieved": round(hbm_achieved, 1),
                 "hbm_frac": round(hbm_achieved / HBM_PEAK_GBS, 4),
                 "traffic_frac": round(traffic_frac, 4) if traffic_frac is not None else None,

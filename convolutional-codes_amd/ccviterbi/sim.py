@@ -313,7 +313,7 @@ def main(argv=None, decode=None):
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None,
                     help="process-group backend (default nccl = RCCL over xGMI)")
     ap.add_argument("--same-device", action="store_true",
-                    help="rehearsal on a one-GPU box: every rank on cuda:0 (use with --backend gloo)")
+                    help="rehearsal on a one-GPU box: every rank on cuda:0, reductions over gloo")
     ap.add_argument("--out", default=None, help="also write the points as a JSON list (rank 0)")
     ap.add_argument("--warmup", type=float, default=0.2,
                     help="seconds of throw-away device-channel chunks before the first point (allocation, "
@@ -336,7 +336,10 @@ def main(argv=None, decode=None):
     if args.noise == "f32" and (channel != SOFT or not args.device_channel):
         raise SystemExit("--noise f32 is an option of the on-device AWGN channel (--device-channel)")
     points = _parse_points(args.points, channel)
-    backend = args.backend or ("gloo" if decode is not None else "nccl")
+    # --same-device puts every rank on cuda:0, which RCCL refuses: gloo then, as in bench.py
+    backend = args.backend or ("gloo" if decode is not None or args.same_device else "nccl")
+    if args.same_device and backend == "nccl" and world > 1:
+        raise SystemExit("--same-device runs every rank on cuda:0, which RCCL (nccl) refuses: use --backend gloo")
 
     import torch
     import torch.distributed as dist

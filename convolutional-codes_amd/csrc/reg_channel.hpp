@@ -3,7 +3,9 @@
 // (AWGN with the opt-in fp32 Box-Muller): two translation units so they compile in parallel.
 #pragma once
 #include <array>
+#include <mutex>
 #include <utility>
+#include <vector>
 
 #include "channel_dev.hpp"
 #include "reg_codes.hpp"
@@ -14,10 +16,22 @@ namespace chan_impl {
 // LDS budget of the decision column array per wave (opt-in kernel): 20 KiB = 8 waves per CU
 constexpr size_t kChanLdsBudget = 20 * 1024;
 
-// Waves per CU of a one-wave-workgroup kernel with `lds` bytes of dynamic LDS.
+// Waves per CU of a one-wave-workgroup kernel with `lds` bytes of dynamic LDS, cached per (kernel,
+// LDS bytes, device): the auto choice below is fixed per instantiation, block length and device, and a
+// sweep launches per chunk (the occupancy queries were paid on every K <= 7 channel launch).
 inline int waves_per_cu(const void* fn, size_t lds) {
+  struct Entry { const void* fn; size_t lds; int dev; int waves; };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Entry& e : cache)
+    if (e.fn == fn && e.lds == lds && e.dev == dev) return e.waves;
   int n = 0;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kRegThreads, lds) == hipSuccess ? n : 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kRegThreads, lds) != hipSuccess) return 0;
+  cache.push_back({fn, lds, dev, n});
+  return n;
 }
 
 // Decisions in LDS only where that costs no occupancy: LDS when its kernel holds at least as many

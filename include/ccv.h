@@ -124,9 +124,11 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
  * d_errors and d_channel (export of the decoder input: float [nb][T][2^n] or uint8 [nb][T]) may be
  * NULL; info and output then go to plan-owned scratch. Info bits and BSC symbols are bit-identical
  * to ccv_sim_*; AWGN samples use the device's double log/sin/cos. AWGN scalings must lie in
- * [0, 2^28) (Eb/N0 above -160 dB), else -1. Asynchronous on `stream`. K = 9 soft codes at blen 40
- * run as two kernels instead: the frames into d_channel (or plan scratch), then the persistent decode
- * (same draws, same results; CCV_CHANNEL_FUSED=1 forces the fused kernel). */
+ * [0, 2^28) (Eb/N0 above -160 dB), else -1. Asynchronous on `stream`. K = 8 / 9 plans -- soft at
+ * blen 40 and every BSC one -- run as two kernels instead: the frames into d_channel (or plan
+ * scratch), then the decode (the persistent kernels for soft, and for BSC through Hamming-distance
+ * rows; same draws, same results); ccv_plan_set_option(plan, "channel_fused", 1) keeps the fused
+ * kernel, and step-major plans always use it. */
 #define CCV_CHANNEL_HARD_DEMAP 1u   /* AWGN: common/hard-demapper.c instead of common/demapper.c */
 /* Frames only, no decode: info bytes into d_info (or plan scratch) and the decoder input into d_channel
  * (required), same draws as above, for ANY plan -- Viterbi, stack or Fano, n <= 3, K <= 64. d_out,

@@ -475,6 +475,31 @@ def test_k9_bsc_through_the_persistent_kernels(torch_cuda, gen):
         assert np.array_equal(out, out2) and np.array_equal(pm, pm2)
 
 
+@pytest.mark.parametrize("gen", [GEN_REF_X86, GEN_TRUE_PARITY], ids=["ref", "true"])
+def test_k9_bsc_reserved_plan_allocates_nothing_on_decode(torch_cuda, gen):
+    """ccv_plan_reserve(max_blocks) sizes everything a decode of up to max_blocks needs -- for K = 9
+    BSC also the Hamming-distance rows (16 B per step, core.hip hard_rows): the decode then
+    runs no hipMalloc (free device memory unchanged), and the result is the unreserved plan's."""
+    torch = torch_cuda
+    c = K9.with_(gen_mode=gen)
+    nb = 25000   # one 1 M-bit frame: 19.2 MB of rows, far above the allocation granularity
+    _, syms = ch.bsc_blocks(c, nb, 50000, 4321)
+    d_in = torch.from_numpy(syms).to("cuda")
+    d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+    # the runtime's own first-launch allocations (code object; the scratch of a kernel with a spill,
+    # per HIP stream and sized by the grid) come from a throw-away plan's decode on the same stream
+    Plan(c, HARD).decode_device(d_in, nb, d_out)
+    plan = Plan(c, HARD)
+    plan.reserve(nb)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    plan.decode_device(d_in, nb, d_out)
+    torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info()[0] >= free0
+    ref, _ = Plan(c, HARD).decode_host(syms)
+    assert np.array_equal(d_out.cpu().numpy(), ref)
+
+
 def test_k9_true_two_lane_kernel_ragged_groups(torch_cuda):
     """The true-parity K = 9 kernel (two lanes per block, acs_multi2.hpp) decodes a ragged batch of
     several rounds of 32-block groups over the resident waves identically to the oracle."""
