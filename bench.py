@@ -613,6 +613,39 @@ def main(argv=None):
                  "note": "same Philox frames generated on the GPU (encoder, mapper, Box-Muller AWGN, "
                          "demapper fused ahead of the ACS)"}
 
+    # informational, Fano soft rate 1/2: the same frames as received points (x, y) from the on-device
+    # channel (CCV_CHANNEL_IQ: 8 instead of 16 bytes per node) decoded with the distances recomputed in
+    # the kernel (option fano_input 1) -- the device sweep's path; same Philox frames, so the same errors
+    fano_iq = None
+    if (rank == 0 and args.decoder == "fano" and not hard and code.n == 2 and code.K <= 32
+            and not args.no_fused_channel):
+        iq_plan = FanoPlan(code, chan).set_option("fano_input", 1)
+        for opt in args.option:
+            name, value = opt.split("=", 1)
+            if name != "fano_input":
+                iq_plan.set_option(name, int(value))
+        iq_plan.reserve(nb)
+        d_iq = torch.empty((nb, code.steps, 2), dtype=torch.float32, device="cuda")
+        d_iinfo = torch.empty_like(d_info)
+        iq_plan.simulate_frames(args.seed, 0, nb, ch.noise_scaling(args.ebn0), d_iq, d_info=d_iinfo,
+                                stream=stream, iq=True)
+        d_ierr = torch.zeros(1, dtype=torch.int64, device="cuda")
+        reps = max(1, args.steps)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        ev[0].record(stream)
+        for _ in range(reps):
+            iq_plan.decode_device(d_iq, nb, d_out, d_info=d_iinfo, d_errors=d_ierr, stream=stream)
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        i_ms = ev[0].elapsed_time(ev[1]) / reps
+        i_err = int(d_ierr.item()) // reps
+        fano_iq = {"mbit_s": round(nb * code.blen / (i_ms * 1e-3) / 1e6, 2), "kernel_ms": round(i_ms, 3),
+                   "errors_per_step": i_err, "same_info_as_host_frames": bool(torch.equal(d_iinfo, d_info)),
+                   "note": "the step's frames as received points from the on-device channel (8 B per node), "
+                           "demapped in the Fano kernel (fano_input 1)"}
+        del d_iq
+
     # the BER-vs-Eb/N0 half of the metric, after the timed region: every rank decodes its shard of
     # each point's frames on the on-device channel, one all-reduce of the counters (RCCL over xGMI)
     curve = None
@@ -767,6 +800,7 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "cpu_baseline_optimized": cpu_opt,
             "fused_channel": fused,
+            **({"fano_received_points": fano_iq} if fano_iq else {}),
             "ber_curve": ({"frames_per_gpu_per_point": curve_frames, "data": "on-device channel "
                            "(Philox, the reference's noise scaling), stream of point k = (seed, k << 40 | block)",
                            **curve} if curve else None),

@@ -25,6 +25,7 @@ FLAG_NO_PERSISTENT = 8      # skip the persistent K <= 7 kernels (A/B)
 CHANNEL_HARD_DEMAP = 1     # include/ccv.h CCV_CHANNEL_HARD_DEMAP
 CHANNEL_FRAMES_ONLY = 2    # include/ccv.h CCV_CHANNEL_FRAMES_ONLY
 CHANNEL_NOISE_F32 = 4      # include/ccv.h CCV_CHANNEL_NOISE_F32 (opt-in fp32 Box-Muller)
+CHANNEL_IQ = 8             # include/ccv.h CCV_CHANNEL_IQ (frames only: received points, not distances)
 
 
 class DecoderError(RuntimeError):
@@ -137,12 +138,13 @@ class Plan:
             raise DecoderError(f"ccv_simulate_device: {_native.last_error()}")
 
     def simulate_frames(self, seed, first_block, nblocks, channel_param, d_channel, d_info=None,
-                        stream=None, hard_demap=False, noise_f32=False):
+                        stream=None, hard_demap=False, noise_f32=False, iq=False):
         """The on-device channel's frames only (ccv_simulate_device with CCV_CHANNEL_FRAMES_ONLY):
         info bytes into d_info and the decoder input into d_channel, no decode; any plan (Viterbi,
-        stack, Fano), any code with n <= 3."""
+        stack, Fano), any code with n <= 3. iq: the received points (float [nb][T][2]) instead of
+        the demapper's distances (CCV_CHANNEL_IQ; a Fano plan decodes them with fano_input 1)."""
         flags = (CHANNEL_FRAMES_ONLY | (CHANNEL_HARD_DEMAP if hard_demap else 0) |
-                 (CHANNEL_NOISE_F32 if noise_f32 else 0))
+                 (CHANNEL_NOISE_F32 if noise_f32 else 0) | (CHANNEL_IQ if iq else 0))
         rc = self._lib.ccv_simulate_device(self._h, int(seed), int(first_block), int(nblocks),
                                            float(channel_param), flags, _ptr(d_info), None, None, None,
                                            _ptr(d_channel), _stream_handle(stream))

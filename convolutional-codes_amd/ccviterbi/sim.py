@@ -107,7 +107,7 @@ class DeviceChannelDecoder:
 
     def __init__(self, code: Code, channel: int, frame_blocks: int, seed: int, device=None,
                  hard_demap=False, decoder: str = "viterbi", chunk_blocks: Optional[int] = None,
-                 noise_f32: bool = False):
+                 noise_f32: bool = False, fano_iq: Optional[bool] = None):
         import torch
 
         from .decoder import Plan
@@ -128,9 +128,16 @@ class DeviceChannelDecoder:
         self.hard_demap = hard_demap
         self.noise_f32 = noise_f32
         self.d_err = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # Fano, soft rate 1/2: the channel writes the received points and the decoder demaps them
+        # (CCV_CHANNEL_IQ + option fano_input 1: half the bytes per node, the same decoder input)
+        if fano_iq is None:
+            fano_iq = decoder == "fano" and channel == SOFT and code.n == 2 and code.K <= 32
+        self.iq = bool(fano_iq) and decoder == "fano"
+        if self.iq:
+            self.seq.set_option("fano_input", 1)
         if self.seq is not None:
             self.seq.reserve(self.chunk)
-            per_block = code.steps * ((1 << code.n) if channel == SOFT else 1)
+            per_block = code.steps * (2 if self.iq else (1 << code.n) if channel == SOFT else 1)
             dt = torch.float32 if channel == SOFT else torch.uint8
             self.d_ch = torch.empty((self.chunk, per_block), dtype=dt, device=self.device)
             self.d_info = torch.empty((self.chunk, code.info_bytes), dtype=torch.uint8, device=self.device)
@@ -170,7 +177,8 @@ class DeviceChannelDecoder:
                                           stream=stream, hard_demap=self.hard_demap, noise_f32=self.noise_f32)
                 continue
             self.seq.simulate_frames(self.seed, first, nb, param, self.d_ch, d_info=self.d_info,
-                                     stream=stream, hard_demap=self.hard_demap, noise_f32=self.noise_f32)
+                                     stream=stream, hard_demap=self.hard_demap, noise_f32=self.noise_f32,
+                                     iq=self.iq)
             self.seq.decode_device(self.d_ch, nb, self.d_out,
                                    d_path_metric=self.d_pm if self.channel == HARD else None,
                                    d_info=self.d_info, d_errors=self.d_err, stream=stream)

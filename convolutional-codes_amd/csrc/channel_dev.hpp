@@ -54,6 +54,8 @@ struct ChanArgs {
   void* ch_out;              // optional export: soft float [nb][T][2^n] / hard uint8 [nb][T]
   int global_decisions;      // K <= 7: 1 decisions through r.dec in HBM, 0 in LDS, -1 by occupancy
   int noise_f32;             // AWGN: the fp32 Box-Muller (CCV_CHANNEL_NOISE_F32, opt-in) instead of double
+  int iq_out;                // frames only (CCV_CHANNEL_IQ): ch_out gets the demapper's input, the received
+                             // point (x, y) as float [nb][T][2], instead of its 2^n distances
 };
 
 // The opt-in fp32 Box-Muller (CCV_CHANNEL_NOISE_F32): the same uniforms k1, k2 / (2^31 - 1) as the
@@ -308,7 +310,7 @@ struct EncoderRT {
 // F32: the opt-in fp32 Box-Muller (CCV_CHANNEL_NOISE_F32) -- a compile-time choice, so the fp32
 // kernels do not hold the double-precision path's registers (108 instead of 157 VGPRs at K = 7 true
 // parity: one more wave per SIMD).
-template <CodeSpec C, bool HARD, class Enc = Encoder<C>, bool F32 = false>
+template <CodeSpec C, bool HARD, class Enc = Encoder<C>, bool F32 = false, bool IQ = false>
 struct ChannelSource {
   static constexpr int NS = 1 << C.n;
   using MT = typename std::conditional<HARD, uint32_t, float>::type;
@@ -356,7 +358,7 @@ struct ChannelSource {
     }
     enc.start(blen);
     out = a.ch_out && owner
-              ? (void*)((char*)a.ch_out + (size_t)block * T * (HARD ? 1 : NS * sizeof(float)))
+              ? (void*)((char*)a.ch_out + (size_t)block * T * (HARD ? 1 : (IQ ? 2 : NS) * sizeof(float)))
               : nullptr;
   }
 
@@ -437,6 +439,10 @@ struct ChannelSource {
       x = sx;
       y = sy;
     }
+    if constexpr (IQ) {   // the demapper's input: the received point (the snapped one with hard_demap)
+      if (out && d.t < T) reinterpret_cast<float2*>(out)[d.t] = make_float2(x, y);
+      return;
+    }
     constexpr float ndx = pts[0] - pts[2], ndy = pts[1] - pts[3];
     constexpr float nd = (ndx * ndx) + (ndy * ndy);
     // the points as compile-time constants (a loop over pts[] reads them from memory), so the
@@ -475,7 +481,7 @@ struct ChannelSource {
     } else {
       const Draw d = draw();
       compute(d, BM);
-      export_soft(d.t, BM);
+      if constexpr (!IQ) export_soft(d.t, BM);
     }
   }
 };
@@ -711,10 +717,10 @@ struct CodeRT {
   int K, gen;
   uint64_t poly[3];
 };
-template <int NP, bool HARD, bool F32 = false>
+template <int NP, bool HARD, bool F32 = false, bool IQ = false>
 __global__ __launch_bounds__(kRegThreads) void channel_frames_rt(ChanArgs a, CodeRT code) {
   constexpr CodeSpec C{NP, 3, {0, 0, 0, 0, 0, 0, 0, 0}, GEN_REF_X86};   // n only: the encoder is RT
-  using Src = ChannelSource<C, HARD, EncoderRT<NP>, F32>;
+  using Src = ChannelSource<C, HARD, EncoderRT<NP>, F32, IQ>;
   using MT = typename Src::MT;
   const int b = blockIdx.x * kRegThreads + threadIdx.x;
   if (b >= a.r.nblocks) return;

@@ -151,6 +151,7 @@ struct ccv_plan {
     int fano_count_moves = 0;        // diagnostics: iterations = moves
     int channel_fused = 0;           // K = 8 / 9 device channel: fused multilane kernel
     int channel_lds_decisions = -1;  // device channel K <= 7: -1 auto (BSC LDS, AWGN HBM), 0, 1
+    int fano_input = 0;              // soft Fano: 0 the demapper's distances, 1 received points (I/Q)
   } opt;
 };
 
@@ -523,6 +524,15 @@ int ccv_plan_set_option(ccv_plan* p, const char* name, long long value) {
     if (n == "fano_order") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.fano_order = (int)value; }
     if (n == "fano_cap") { if (need(in(-1, 0xFFFFFFFFll), "-1 (default) or moves")) return -1; p->opt.fano_cap = value; }
     if (n == "fano_count_moves") { if (need(in(0, 1), "0 / 1")) return -1; p->opt.fano_count_moves = (int)value; }
+    return 0;
+  }
+  if (n == "fano_input") {   // soft Fano: received points (ccv_simulate_device CCV_CHANNEL_IQ frames)
+    if (need(p->fano, "a Fano-decoder plan option")) return -1;
+    if (need(in(0, 1), "0 distances / 1 received points")) return -1;
+    if (value == 1 && need(p->d.channel == CCV_SOFT && p->d.n == 2 && p->d.K <= 32,
+                           "received points: soft rate-1/2 codes with K <= 32"))
+      return -1;
+    p->opt.fano_input = (int)value;
     return 0;
   }
   if (n == "channel_fused" || n == "channel_lds_decisions") {
@@ -904,6 +914,7 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
     a.park_flags = reinterpret_cast<uint8_t*>(base + hdr + met);
   }
   a.count_moves = p->opt.fano_count_moves;
+  a.iq = p->opt.fano_input;   // before the queue order: its score kernel reads the input too
   // the expected-symbol table: hard input only. For soft input the table load sits in each move's
   // dependent chain next to the row load, and the kernel waits on memory (PMC, round 4: wait 0.66 of
   // wave time, valu_frac 0.17): the ~25 VALU of parities are cheaper (4 dB: 49.6 -> 57.7 Mbit/s, with
@@ -1025,6 +1036,8 @@ static int simulate_frames_only(ccv_plan* p, uint64_t seed, uint64_t first_block
   a.p_ppm = hard ? (int32_t)channel_param : 0;
   a.hard_demap = (channel_flags & CCV_CHANNEL_HARD_DEMAP) != 0;
   a.noise_f32 = (channel_flags & CCV_CHANNEL_NOISE_F32) != 0;
+  a.iq_out = (channel_flags & CCV_CHANNEL_IQ) != 0;
+  if (hard && a.iq_out) return fail("CCV_CHANNEL_IQ: received points belong to the AWGN channel");
   a.info_out = d_info;
   a.ch_out = d_channel;
   HIP_TRY(ccv::launch_channel_frames_any(a, p->d.n, p->d.K, p->polys, p->d.gen_mode, hard, stream));
@@ -1039,6 +1052,7 @@ int ccv_simulate_device(ccv_plan* p, uint64_t seed, uint64_t first_block, size_t
   if (channel_flags & CCV_CHANNEL_FRAMES_ONLY)
     return simulate_frames_only(p, seed, first_block, nblocks, channel_param, channel_flags, d_info,
                                 d_channel, stream_v);
+  if (channel_flags & CCV_CHANNEL_IQ) return fail("CCV_CHANNEL_IQ is an output of CCV_CHANNEL_FRAMES_ONLY");
   if (p->stack || p->fano)
     return fail("a sequential-decoder plan takes the on-device channel with CCV_CHANNEL_FRAMES_ONLY");
   if (!register_path(*p))

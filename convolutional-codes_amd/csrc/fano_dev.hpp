@@ -40,6 +40,7 @@
 
 #include <type_traits>
 
+#include "channel_dev.hpp"
 #include "stack_dev.hpp"
 #include "trellis.hpp"
 
@@ -74,6 +75,8 @@ struct FanoArgs {
   void* park_metric;         // [nb][T + 1] path metrics of the nodes 0..frontier
   uint8_t* park_flags;       // [nb][T + 1] sel | dec << 1 of the nodes 0..frontier
   int rows_mode;             // host only (ccv_plan_set_option "fano_rows"): -1 auto, else kRows*
+  int iq;                    // host only (option "fano_input" 1): `in` holds the received points, float
+                             // [nb][T][2] (ccv_simulate_device CCV_CHANNEL_IQ), demapped in the kernel
 };
 
 constexpr int kFanoParkWords = 12;
@@ -94,6 +97,38 @@ __global__ void fano_score(const float* in, int T, int nblocks, float* key, uint
     float m = p[t * NS];
 #pragma unroll
     for (int k = 1; k < NS; ++k) m = fminf(m, p[t * NS + k]);
+    s += m;
+  }
+  key[b] = s;
+  idx[b] = (uint32_t)b;
+}
+
+// distance of the received point (x, y) to QPSK point e, as the demapper computes it (the points
+// (+-a, +-a): x negative for symbol bit 1, y for bit 0 -- channel_dev.hpp's sign flips; no contraction:
+// the translation unit is built with -ffp-contract=off)
+__device__ __forceinline__ float qpsk_distance(float x, float y, uint32_t e) {
+  constexpr const float* pts = Constellation<2>::pts;
+  static_assert(pts[0] == pts[1] && pts[4] == -pts[0] && pts[3] == -pts[1], "QPSK signs");
+  constexpr float ndx = pts[0] - pts[2], ndy = pts[1] - pts[3];
+  constexpr float nd = (ndx * ndx) + (ndy * ndy);
+  const uint32_t a = __builtin_bit_cast(uint32_t, pts[0]);
+  const float px = __builtin_bit_cast(float, a ^ ((e & 2u) << 30)), py = __builtin_bit_cast(float, a ^ ((e & 1u) << 31));
+  return div_const<nd>(((x - px) * (x - px)) + ((y - py) * (y - py)));
+}
+
+// The same score from received points (option "fano_input" 1): the nearest point's distance, the
+// demapper's arithmetic -- the order, and so the schedule, of the distance-row input.
+template <int NP = 2>   // a template: the header is in two translation units
+__global__ void fano_score_iq(const float* in, int T, int nblocks, float* key, uint32_t* idx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const float2* p = reinterpret_cast<const float2*>(in) + (size_t)b * T;
+  float s = 0.0f;
+  for (int t = 0; t < T; ++t) {
+    const float2 v = p[t];
+    float m = qpsk_distance(v.x, v.y, 0u);
+#pragma unroll
+    for (uint32_t k = 1; k < 4; ++k) m = fminf(m, qpsk_distance(v.x, v.y, k));
     s += m;
   }
   key[b] = s;
@@ -122,8 +157,14 @@ __host__ __device__ constexpr size_t fano_node_bytes(int T, size_t metric_bytes)
 //   kRowsLds: as kRowsGlobal, the block's rows copied into LDS when the lane takes the block.
 // (Round 5 measured and removed a register window of rows cur - 1, cur, cur + 1 with one load per
 // move issued a pass ahead: 67 -> 48 Mbit/s soft, 222 -> 156 BSC, profiles/r05b/.)
-constexpr int kRowsDirect = 0, kRowsGlobal = 2, kRowsLds = 1;
-template <bool HARD, int NP>
+//   kRowsIQ / kRowsIQLds (round 6, soft rate 1/2, option "fano_input" 1): the rows are the received
+//     points (x, y) -- 8 instead of 16 bytes per node -- from global memory as kRowsGlobal, or in LDS;
+//     the two branch metrics are the demapper's distances recomputed with its exact fp32 operations
+//     (common/demapper.c:66-70 as channel_dev.hpp ChannelSource::compute): the same decoder input bit
+//     for bit, for frames the on-device channel produced (a drop-in caller's input IS the distances).
+constexpr int kRowsDirect = 0, kRowsGlobal = 2, kRowsLds = 1, kRowsIQ = 3, kRowsIQLds = 4;
+constexpr bool rows_iq(int rm) { return rm == kRowsIQ || rm == kRowsIQLds; }
+template <bool HARD, int NP, bool IQ = false>
 struct FanoRow;
 template <int NP>
 struct FanoRow<true, NP> {
@@ -134,7 +175,15 @@ struct FanoRow<true, NP> {
   }
 };
 template <int NP>
-struct FanoRow<false, NP> {
+struct FanoRow<false, NP, true> {
+  float2 v;
+  __device__ void pick(bool a, const FanoRow& ra, bool b, const FanoRow& rb) {
+    v.x = a ? ra.v.x : (b ? rb.v.x : v.x);
+    v.y = a ? ra.v.y : (b ? rb.v.y : v.y);
+  }
+};
+template <int NP>
+struct FanoRow<false, NP, false> {
   float4 v;
   __device__ void pick(bool a, const FanoRow& ra, bool b, const FanoRow& rb) {
     v.x = a ? ra.v.x : (b ? rb.v.x : v.x);
@@ -158,15 +207,19 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   using ET = typename std::conditional<HARD, uint8_t, float>::type;
   using ST = typename std::conditional<W32, uint32_t, uint64_t>::type;
   static_assert(RM == kRowsDirect || HARD || NP == 2, "rows of received symbols are a byte or a float4");
+  static_assert(!rows_iq(RM) || (!HARD && NP == 2), "received points: soft rate 1/2");
   constexpr bool ROWS = RM != kRowsDirect;
+  constexpr bool IQ = rows_iq(RM);
+  constexpr bool LDSROWS = RM == kRowsLds || RM == kRowsIQLds;
+  using Row = FanoRow<HARD, NP, IQ>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   const int T = a.T, K = a.K, n = a.n;
-  const int NS = HARD ? 1 : (1 << n);
+  const int NS = HARD ? 1 : (IQ ? 2 : (1 << n));   // input floats per node
   // node arrays [T + 1][64]; row T takes the stores a lane does not need
   MT* metric = reinterpret_cast<MT*>(smem);
   uint8_t* flags = smem + (size_t)(T + 1) * kFanoThreads * sizeof(MT);   // sel | dec << 1
-  // rows: [T][64] float4 (soft) or bytes (hard), after the flags (16-byte aligned)
+  // rows: [T][64] float4 / float2 (soft) or bytes (hard), after the flags (16-byte aligned)
   unsigned char* rows = smem + fano_node_bytes(T, sizeof(MT));
   // a node's flags byte (sel | dec << 1)
   auto flag_get = [&](int d) -> uint32_t { return flags[d * kFanoThreads + lane]; };
@@ -185,19 +238,21 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
 
   const ET* rx = nullptr;
   auto row_at = [&](int d) {
-    FanoRow<HARD, NP> r;
-    if constexpr (RM == kRowsLds) {
+    Row r;
+    if constexpr (LDSROWS) {
       if constexpr (HARD) r.v = rows[d * kFanoThreads + lane];
+      else if constexpr (IQ) r.v = reinterpret_cast<const float2*>(rows)[d * kFanoThreads + lane];
       else r.v = reinterpret_cast<const float4*>(rows)[d * kFanoThreads + lane];
     } else {
       if constexpr (HARD) r.v = rx[d];
+      else if constexpr (IQ) r.v = reinterpret_cast<const float2*>(rx)[d];
       else r.v = reinterpret_cast<const float4*>(rx)[d];
     }
     return r;
   };
   // get_transition_metric + sort (:160-181, :213-236) for the node at depth d with state st, whose
   // received row is `row` (ROWS): tm0 >= tm1 afterwards, swapped = input 1 is the best branch
-  auto node_metrics = [&](const ET* rx, int d, ST st, const FanoRow<HARD, NP>& row, MT& tm0, MT& tm1,
+  auto node_metrics = [&](const ET* rx, int d, ST st, const Row& row, MT& tm0, MT& tm1,
                           uint32_t& swapped) {
     uint32_t es;
     if constexpr (TAB) es = a.symtab[(uint32_t)st];
@@ -211,7 +266,10 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       t1 = d1 * a.bm1 + (n - d1) * a.bm0;
     } else {
       float r0, r1;
-      if constexpr (ROWS || NP == 2) {   // rate 1/2: the node's whole row is one 16-byte load
+      if constexpr (IQ) {   // the demapper's two distances from the received point
+        r0 = qpsk_distance(row.v.x, row.v.y, e0);
+        r1 = qpsk_distance(row.v.x, row.v.y, e1);
+      } else if constexpr (ROWS || NP == 2) {   // rate 1/2: the node's whole row is one 16-byte load
         const float4 v = ROWS ? row.v : reinterpret_cast<const float4*>(rx)[d];
         r0 = (e0 & 2u) ? ((e0 & 1u) ? v.w : v.z) : ((e0 & 1u) ? v.y : v.x);
         r1 = (e1 & 2u) ? ((e1 & 1u) ? v.w : v.z) : ((e1 & 1u) ? v.y : v.x);
@@ -252,7 +310,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   uint32_t sel = 0, dec = 0, timeout = 0;
   bool inback = false, moved = false;
   uint32_t moves = 0, spass = 0;
-  FanoRow<HARD, NP> row0{};   // received row of node cur
+  Row row0{};   // received row of node cur
   auto as_bits = [](MT v) -> uint32_t {
     if constexpr (HARD) return (uint32_t)v;
     else return __float_as_uint(v);
@@ -289,9 +347,13 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   };
   auto load_rows = [&]() {
     rx = in + (size_t)b * T * NS;
-    if constexpr (RM == kRowsLds) {
+    if constexpr (LDSROWS) {
       if constexpr (HARD) {
         for (int d = 0; d < T; ++d) rows[d * kFanoThreads + lane] = rx[d];
+      } else if constexpr (IQ) {
+        const float2* src = reinterpret_cast<const float2*>(rx);
+        float2* dst = reinterpret_cast<float2*>(rows);
+        for (int d = 0; d < T; ++d) dst[d * kFanoThreads + lane] = src[d];
       } else {
         const float4* src = reinterpret_cast<const float4*>(rx);
         float4* dst = reinterpret_cast<float4*>(rows);
@@ -400,7 +462,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     const MT mprev = metric[cm * kFanoThreads + lane];
     const uint32_t fprev = flag_get(cm);
     const uint32_t fold = flag_get(cur >= K ? cur - K : 0);
-    FanoRow<HARD, NP> rowm{}, rowp{};
+    Row rowm{}, rowp{};
     if constexpr (ROWS) {
       rowm = row_at(cm);
       rowp = row_at(cur + 1 < T ? cur + 1 : T - 1);

@@ -76,6 +76,17 @@ hipError_t launch_frames(const ChanArgs& a, int grid, hipStream_t stream) {
 template <bool HARD, bool F32>
 hipError_t launch_frames_rt(const ChanArgs& a, int n, const CodeRT& code, hipStream_t stream) {
   const dim3 grid((unsigned)((a.r.nblocks + kRegThreads - 1) / kRegThreads)), block(kRegThreads);
+  if constexpr (!HARD) {
+    if (a.iq_out) {   // the received points instead of the distances (CCV_CHANNEL_IQ)
+      switch (n) {
+        case 1: hipLaunchKernelGGL((channel_frames_rt<1, false, F32, true>), grid, block, 0, stream, a, code); break;
+        case 2: hipLaunchKernelGGL((channel_frames_rt<2, false, F32, true>), grid, block, 0, stream, a, code); break;
+        case 3: hipLaunchKernelGGL((channel_frames_rt<3, false, F32, true>), grid, block, 0, stream, a, code); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+  }
   switch (n) {
     case 1: hipLaunchKernelGGL((channel_frames_rt<1, HARD, F32>), grid, block, 0, stream, a, code); break;
     case 2: hipLaunchKernelGGL((channel_frames_rt<2, HARD, F32>), grid, block, 0, stream, a, code); break;

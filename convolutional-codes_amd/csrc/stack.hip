@@ -148,6 +148,10 @@ static hipError_t launch_fano_v(const FanoArgs& a, size_t lds, hipStream_t s) {
 template <bool HARD>
 static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream_t s) {
   if (a.K <= 32 && a.n == 2) {
+    if constexpr (!HARD) {
+      if (rm == kRowsIQ) return launch_fano_v<false, 2, true, kRowsIQ>(a, lds, s);
+      if (rm == kRowsIQLds) return launch_fano_v<false, 2, true, kRowsIQLds>(a, lds, s);
+    }
     if (rm == kRowsLds) return launch_fano_v<HARD, 2, true, kRowsLds>(a, lds, s);
     if (rm == kRowsGlobal) return launch_fano_v<HARD, 2, true, kRowsGlobal>(a, lds, s);
     return launch_fano_v<HARD, 2, true, kRowsDirect>(a, lds, s);
@@ -170,8 +174,16 @@ static hipError_t launch_fano_h(const FanoArgs& a, int rm, size_t lds, hipStream
 // parities computed instead of the table load (profiles/r04c/fano_ab.txt). Soft K=15 rows in LDS
 // (16 B per node) cut the chip from 9 to 2 waves per CU and run 4x slower. The plan option
 // "fano_rows" (FanoArgs::rows_mode) overrides.
+// Received points (option "fano_input" 1, soft rate 1/2, K <= 32): half-size rows prefetched from
+// global memory (kRowsIQ), or in LDS with "fano_rows" 1 (kRowsIQLds).
 hipError_t launch_fano(const FanoArgs& a, bool hard, hipStream_t s) {
   const size_t node_bytes = fano_node_bytes(a.T, hard ? sizeof(int32_t) : sizeof(float));
+  if (a.iq) {
+    if (hard || a.n != 2 || a.K > 32) return hipErrorInvalidValue;
+    const bool lds_rows = a.rows_mode == kRowsLds || a.rows_mode == kRowsIQLds;
+    const size_t lds = node_bytes + (lds_rows ? (size_t)a.T * kFanoThreads * 8 : 0);
+    return launch_fano_h<false>(a, lds_rows ? kRowsIQLds : kRowsIQ, lds, s);
+  }
   const size_t row_bytes = (size_t)a.T * kFanoThreads * (hard ? 1 : 16);
   const bool rowable = hard || (a.n == 2 && a.K <= 32);
   int rm = hard ? kRowsLds : (rowable ? kRowsGlobal : kRowsDirect);
@@ -193,7 +205,7 @@ size_t fano_order_bytes(int nblocks) {
 }
 
 static hipError_t noise_order(const void* in_v, int n_out, int T, int nblocks, void* scratch, size_t bytes,
-                              const uint32_t** order, hipStream_t s) {
+                              const uint32_t** order, hipStream_t s, bool iq = false) {
   const size_t n = (size_t)nblocks;
   float* k_in = static_cast<float*>(scratch);
   float* k_out = k_in + n;
@@ -203,7 +215,9 @@ static hipError_t noise_order(const void* in_v, int n_out, int T, int nblocks, v
   size_t tmp_bytes = bytes - (size_t)(static_cast<char*>(tmp) - static_cast<char*>(scratch));
   const float* in = static_cast<const float*>(in_v);
   const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  if (n_out == 2) hipLaunchKernelGGL((fano_score<4>), grid, block, 0, s, in, T, nblocks, k_in, i_in);
+  if (iq && n_out == 2) hipLaunchKernelGGL(fano_score_iq<2>, grid, block, 0, s, in, T, nblocks, k_in, i_in);
+  else if (iq) return hipErrorInvalidValue;
+  else if (n_out == 2) hipLaunchKernelGGL((fano_score<4>), grid, block, 0, s, in, T, nblocks, k_in, i_in);
   else if (n_out == 3) hipLaunchKernelGGL((fano_score<8>), grid, block, 0, s, in, T, nblocks, k_in, i_in);
   else return hipErrorInvalidValue;
   hipError_t e = hipGetLastError();
@@ -216,7 +230,7 @@ static hipError_t noise_order(const void* in_v, int n_out, int T, int nblocks, v
 
 hipError_t launch_fano_order(const FanoArgs& a, void* scratch, size_t bytes, const uint32_t** order,
                              hipStream_t s) {
-  return noise_order(a.in, a.n, a.T, a.nblocks, scratch, bytes, order, s);
+  return noise_order(a.in, a.n, a.T, a.nblocks, scratch, bytes, order, s, a.iq != 0);
 }
 
 }  // namespace ccv

@@ -139,6 +139,12 @@ int ccv_decode_device(ccv_plan* plan, const void* d_in, size_t nblocks, uint8_t*
  * draw order) instead of double precision. Faster; the samples are NOT bit-identical to the double
  * path or glibc (a few fp32 ulp, tools/chanmath_f32_check.hip), so only the BER statistics match. */
 #define CCV_CHANNEL_NOISE_F32 4u
+/* Frames only, AWGN (round 6): d_channel gets the demapper's INPUT -- the received point (x, y), float
+ * [nb][T][2], after the hard demapper's snap with CCV_CHANNEL_HARD_DEMAP -- instead of its 2^n
+ * distances. A Fano plan with option "fano_input" 1 decodes such frames, recomputing the distances with
+ * the demapper's exact fp32 operations (common/demapper.c:66-70): the same decoder input bit for bit,
+ * in half the bytes per node (n = 2). */
+#define CCV_CHANNEL_IQ 8u
 int ccv_simulate_device(ccv_plan* plan, uint64_t seed, uint64_t first_block, size_t nblocks,
                         double channel_param, unsigned channel_flags, uint8_t* d_info, uint8_t* d_out,
                         int32_t* d_path_metric, unsigned long long* d_errors, void* d_channel,
@@ -202,6 +208,9 @@ int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out
  *                 "fano_order"       1 noisiest blocks first for soft input (default), 0 natural order
  *                 "fano_cap"         -1 default (4000 x T moves), 0 one pass, else moves before parking
  *                 "fano_count_moves" 1: d_iterations gets moves instead of timeout ticks (diagnostics)
+ *                 "fano_input"       0 the demapper's distances (default: the reference decoder's input),
+ *                                    1 received points float [nb][T][2] (CCV_CHANNEL_IQ frames; soft,
+ *                                    n = 2, K <= 32); "fano_rows" 1 then keeps the points in LDS
  *   Viterbi plans (on-device channel):
  *                 "channel_fused"    1: K = 8 / 9 codes use the fused multilane channel kernel
  *                 "channel_lds_decisions"  -1 auto (LDS unless it costs occupancy), 0 HBM, 1 LDS (K <= 7) */

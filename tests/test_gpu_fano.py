@@ -211,3 +211,60 @@ def test_reference_driver_with_mi355x_fano_decoder(case, tmp_path):
         assert np.array_equal(np.fromfile(prefix + ".pm", dtype=np.int32), g["path_metric"])
     meta = dict(line.split() for line in open(prefix + ".meta"))
     assert int(meta["errors"]) == case["errors"]
+
+
+@pytest.mark.parametrize("hard_demap", [False, True], ids=["demap", "hard_demap"])
+@pytest.mark.parametrize("rows", [-1, 1], ids=["iq_global", "iq_lds"])
+def test_fano_received_points_equal_distance_rows(torch_cuda, rows, hard_demap):
+    """Device sweeps of the Fano decoder (round 6): the channel writes the received points (x, y)
+    (CCV_CHANNEL_IQ) and the kernel demaps them with the demapper's exact fp32 operations (option
+    fano_input 1; points prefetched from global memory, or in LDS with fano_rows 1). Same seed, same
+    frames: the demapped points equal the channel's distance frames bit for bit (recomputed on the
+    host in numpy fp32 as common/demapper.c:66-70), and the decode -- outputs, error count, every
+    block's search length, two-pass parking included -- equals the distance-row decode (K = 15 at
+    2 dB: long searches and timeouts)."""
+    torch = torch_cuda
+    c, nb, seed = K15, 1500, 77
+    param = ch.noise_scaling(2.0)
+    dist_plan = FanoPlan(c, SOFT)
+    iq_plan = FanoPlan(c, SOFT).set_option("fano_input", 1).set_option("fano_rows", rows)
+    d_dist = torch.empty((nb, c.steps, 4), dtype=torch.float32, device="cuda")
+    d_iq = torch.empty((nb, c.steps, 2), dtype=torch.float32, device="cuda")
+    d_info = torch.empty((nb, c.info_bytes), dtype=torch.uint8, device="cuda")
+    d_info2 = torch.empty_like(d_info)
+    dist_plan.simulate_frames(seed, 5 << 40, nb, param, d_dist, d_info=d_info, hard_demap=hard_demap)
+    iq_plan.simulate_frames(seed, 5 << 40, nb, param, d_iq, d_info=d_info2, hard_demap=hard_demap, iq=True)
+    torch.cuda.synchronize()
+    assert torch.equal(d_info, d_info2)
+    xy = d_iq.cpu().numpy()
+    a = np.float32(0.707107)
+    nd = np.float32(np.float32(a - (-a)) * np.float32(a - (-a)))   # (dx*dx) + (dy*dy) with dx = 0
+    host = np.empty((nb, c.steps, 4), np.float32)
+    for e in range(4):
+        px = np.float32(-a if e & 2 else a)
+        py = np.float32(-a if e & 1 else a)
+        dx = xy[..., 0] - px
+        dy = xy[..., 1] - py
+        host[..., e] = ((dx * dx) + (dy * dy)) / nd
+    assert np.array_equal(host.view(np.uint32), d_dist.cpu().numpy().view(np.uint32))
+    runs = []
+    for plan, d_in in ((dist_plan, d_dist), (iq_plan, d_iq)):
+        d_out = torch.empty((nb, c.out_bytes), dtype=torch.uint8, device="cuda")
+        d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+        d_it = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        plan.decode_fano_device(d_in, nb, d_out, d_info=d_info, d_errors=d_err, d_iterations=d_it)
+        torch.cuda.synchronize()
+        runs.append((d_out.cpu().numpy(), int(d_err.item()), d_it.cpu().numpy()))
+    (o0, e0, i0), (o1, e1, i1) = runs
+    assert np.array_equal(o0, o1) and e0 == e1 and np.array_equal(i0, i1)
+    assert (i0 == 10000 * c.steps).any()   # timeouts in the batch
+    assert e0 == ch.count_bit_errors(c, d_info.cpu().numpy(), o0)
+
+
+def test_fano_received_points_option_limits():
+    """fano_input 1 is for soft rate-1/2 Fano plans with K <= 32; received points belong to AWGN."""
+    with pytest.raises(Exception, match="received points"):
+        FanoPlan(K15, HARD).set_option("fano_input", 1)
+    with pytest.raises(Exception, match="Fano"):
+        from ccviterbi import Plan, K7
+        Plan(K7, SOFT).set_option("fano_input", 1)
