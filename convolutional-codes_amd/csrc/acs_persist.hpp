@@ -372,8 +372,16 @@ enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, 
 // Production schedules (round 6, tools/tail_bench.hip, profiles/r06c): the group queue with full
 // stealing -- soft 0.982x the static walk's time, hard 0.869x (+ the info loads ahead of the DMA, 0.997x
 // alone); 0, 1 or 7 steal hops measured alike.
+// K = 7 only: a group of a smaller code is over in a few microseconds, about a ticket's round trip,
+// and its dequeue rate exceeds the heads' (code 0, K = 3, BSC: 40,625 groups in 0.104 ms = 390
+// dequeues/us; on the queue 0.104 -> 0.167 ms per launch, profiles/r06_bench) -- those keep the
+// static walk.
 constexpr int kPersistSoftProd = kPersistQueue | kPersistQueueHop7;
 constexpr int kPersistHardProd = kPersistQueue | kPersistQueueHop7 | kPersistInfoFirst;
+template <CodeSpec C>
+constexpr int persist_soft_opt() { return C.K >= 7 ? kPersistSoftProd : 0; }
+template <CodeSpec C>
+constexpr int persist_hard_opt() { return C.K >= 7 ? kPersistHardProd : 0; }
 static_assert(kPersistQueue == 1024, "GroupWalk::QUEUE");
 // steal hops of the queue schedule (GroupQueue::resolve): 0, or the OPT bits above
 constexpr int queue_hops(int opt) {

@@ -1,6 +1,6 @@
 // reg_persist.hip -- ahead-of-time instantiation of the persistent K <= 7 register-trellis kernels
 // (acs_persist.hpp) for the codes in reg_codes.hpp: soft for r = 1/2 codes, hard for every code; both
-// on the group queue (RegArgs::queue, the plan's), kPersistSoftProd / kPersistHardProd.
+// on the group queue (RegArgs::queue, the plan's) at K = 7, the static walk for smaller codes (persist_*_opt).
 #include <array>
 #include <utility>
 
@@ -16,7 +16,7 @@ constexpr bool kSoftOk = kRegCodes[I].n == 2;
 template <size_t I>
 hipError_t launch_soft(const RegArgs& a, int ngroups, hipStream_t stream) {
   if constexpr (kSoftOk<I>) {
-    return launch_persistent(viterbi_soft_persist<kRegCodes[I], kPersistBlen, kPersistSoftProd>, a, ngroups, stream);
+    return launch_persistent(viterbi_soft_persist<kRegCodes[I], kPersistBlen, persist_soft_opt<kRegCodes[I]>()>, a, ngroups, stream);
   } else {
     return hipErrorInvalidValue;
   }
@@ -24,7 +24,7 @@ hipError_t launch_soft(const RegArgs& a, int ngroups, hipStream_t stream) {
 
 template <size_t I>
 hipError_t launch_hard(const RegArgs& a, int ngroups, hipStream_t stream) {
-  return launch_persistent(viterbi_hard_persist<kRegCodes[I], kPersistBlen, 3, kPersistHardProd>, a, ngroups,
+  return launch_persistent(viterbi_hard_persist<kRegCodes[I], kPersistBlen, 3, persist_hard_opt<kRegCodes[I]>()>, a, ngroups,
                            stream);
 }
 
