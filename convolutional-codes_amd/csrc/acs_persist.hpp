@@ -388,8 +388,13 @@ constexpr int queue_hops(int opt) {
   return (opt & kPersistQueueHop7) ? kQueueLabels - 1 : (opt & kPersistQueueHop1) ? 1 : 0;
 }
 
+// CCV_PERSIST_SOFT_WAVES (A/B builds only): the soft kernel's minimum waves per SIMD (2 in production:
+// 195 VGPRs; 3 caps it at 168 and spills, 4.5 % slower on the static walk in round 5)
+#ifndef CCV_PERSIST_SOFT_WAVES
+#define CCV_PERSIST_SOFT_WAVES 2
+#endif
 template <CodeSpec C, int BLEN, int ABLATE = 0>
-__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(kRegThreads) __attribute__((amdgpu_waves_per_eu(CCV_PERSIST_SOFT_WAVES)))
 void viterbi_soft_persist(RegArgs a, int ngroups) {
   constexpr int S = 1 << (C.K - 1);
   static_assert(C.n == 2, "16-byte trellis steps");

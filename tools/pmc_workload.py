@@ -129,11 +129,12 @@ def main():
     for a, d in (("--code", None), ("--frames", "104"), ("--layout", "block"), ("--channel", "awgn"),
                  ("--decoder", "viterbi"), ("--ebn0", "4.0"), ("--p-ppm", "50000"), ("--reps", "3")):
         ap.add_argument(a, default=d)
+    ap.add_argument("--iq", action="store_true")
     args = ap.parse_args(sys.argv[3:])
     args.code = args.code or ("k7" if args.decoder == "viterbi" else "k15")
     args.frames = int(args.frames)
     import bench
-    key = bench.workload_key_of(args)
+    key = bench.workload_key_of(args) + (":iq" if args.iq else "")
     fetch, durs = counters(os.path.join(root, "FETCH"))
     write, _ = counters(os.path.join(root, "WRITE"))
     sq, sq_durs = counters(os.path.join(root, "SQ"))

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0xC0DE)
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE")
+    ap.add_argument("--iq", action="store_true",
+                    help="Fano, soft: the frames as received points from the on-device channel, decoded "
+                         "with option fano_input 1 (bench.py fano_received_points)")
     args = ap.parse_args()
     import torch
 
@@ -44,6 +47,8 @@ def main():
     for _ in range(args.reps):
         dst.copy_(d_rx)
     torch.cuda.synchronize()
+    copy_bytes = d_rx.numel() * d_rx.element_size()
+    del dst
     d_out = torch.empty((nb, code.out_bytes), dtype=torch.uint8, device="cuda")
     d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
     chan = HARD if hard else SOFT
@@ -56,11 +61,15 @@ def main():
     for opt in args.option:
         name, value = opt.split("=", 1)
         plan.set_option(name, int(value))
+    if args.iq:   # the same Philox frames, as received points
+        plan.set_option("fano_input", 1)
+        d_rx = torch.empty((nb, code.steps, 2), dtype=torch.float32, device="cuda")
+        plan.simulate_frames(args.seed, 0, nb, ch.noise_scaling(args.ebn0), d_rx, d_info=d_info, iq=True)
     plan.reserve(nb)
     for _ in range(args.reps):
         plan.decode_device(d_rx, nb, d_out, d_info=d_info, d_errors=d_err, stream=torch.cuda.current_stream())
     torch.cuda.synchronize()
-    print("copy_bytes", d_rx.numel() * d_rx.element_size(), "nblocks", nb)
+    print("copy_bytes", copy_bytes, "nblocks", nb)
 
 
 if __name__ == "__main__":
