@@ -292,20 +292,18 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
       // this chunk's DMA was issued before the previous period's 8 decision stores (in order)
       if (p >= 2) wait_vmcnt<n>();
       else wait_vmcnt<0>();
-      if constexpr (GROWTH) {
-        const int bc = blk < nb ? blk : nb - 1;
-#pragma unroll
-        for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
-        asm volatile("" ::: "memory");   // info loads before the DMA (vmcnt order)
-      }
+      // the next group from the ticket fetched a group ago, read right behind this full drain (see
+      // acs_wide.hpp)
+      if constexpr (GROWTH) nxt = walk.next(g);
       const int buf = p & 1;
       if (p + 1 < NPER) {
         issue_chunk(g, p + 1, buf ^ 1);
       } else {   // the next group's first chunk (a harmless reload of this one's when there is none)
-        nxt = walk.next(g);
         issue_chunk(nxt < ngroups ? nxt : g, 0, buf ^ 1);
-        walk.issued(nxt);
       }
+      // the ticket after nxt: behind the info loads, whose unpacking waits vmcnt(0) right away, and
+      // the DMA; waited by period 1's full drain, long back by then
+      if constexpr (GROWTH) walk.issued(nxt);
       const uint32_t rd = row + (uint32_t)(buf * BUF);
       f32x4 rowv = lds_read_b128<0>(rd + swz);
       auto phase_at = [&]<int P>() __attribute__((always_inline)) {
@@ -363,6 +361,14 @@ void viterbi_multi2_slot(RegArgs a, int ngroups) {
     uint64_t h = st;
     const uint32_t qself = (uint32_t)q;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this group's decision stores reached L2
+    // the transmitted info bytes, loaded here (round 6) rather than at the growth period, where their
+    // unpacking waited vmcnt(0) at once -- for the period's DMA and the queue ticket as well; here
+    // they return behind the traceback's loads
+    {
+      const int bc = blk < nb ? blk : nb - 1;
+#pragma unroll
+      for (int k = 0; k < IB; ++k) info[k] = info_src[(size_t)bc * info_stride + k];
+    }
     u32x4 dw[2][n];
     auto load_period = [&]<int pp>() __attribute__((always_inline)) {   // main period pp (1-based)
 #pragma unroll

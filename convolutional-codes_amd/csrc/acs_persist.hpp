@@ -231,6 +231,9 @@ struct GroupQueue {
   // (A snapshot of the other heads in the same instruction -- lanes 1..7 adding 0 -- multiplies the
   // atomic traffic per head by 8, past one word's ~88/us ceiling: 1.27-1.46x the static walk's time,
   // profiles/r06b.)
+  // (Leaving the other lanes' t undefined instead of 0 -- the zero's v_mov into the register the
+  // previous fetch returned into makes hipCC drain the stores in flight first, inside the K = 9
+  // kernels' chunk loop -- let the optimizer break the kernels: wrong outputs, profiles/r06_tail/r06j.)
   __device__ __forceinline__ uint32_t fetch(int x, int lane) const {
     uint32_t z;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));

@@ -315,13 +315,18 @@ void viterbi_wide_persist(RegArgs a, int ngroups) {
       // complete in order, so vmcnt(16) is its landing (chunks 0 and 1 follow no stores)
       if ((ABLATE & 1) == 0 && c >= 2) wait_vmcnt<16>();
       else wait_vmcnt<0>();
+      // the next group from the ticket fetched a group ago: read right behind this full drain (the
+      // growth chunk's), not at the last chunk, where it would drain the previous chunk's decision
+      // stores that the counted vmcnt(16) leaves in flight
+      if constexpr (GROWTH) {
+        nxt = walk.next(g);
+        walk.issued(nxt);   // the ticket after it, here too: waited by chunk 1's full drain, long back
+      }
       const int buf = c & 1;
       if (c + 1 < NCH) {
         issue_chunk(g, c + 1, buf ^ 1);
       } else {   // the next group's first chunk (a harmless reload of this one's when there is none)
-        nxt = walk.next(g);
         issue_chunk(nxt < ngroups ? nxt : g, 0, buf ^ 1);
-        walk.issued(nxt);
       }
       const uint32_t rd = rd_base + (uint32_t)(buf * BUF);
       f32x4 row = lds_read_b128<0>(rd);
