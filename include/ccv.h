@@ -20,6 +20,10 @@
  * Not thread-safe per plan: use one plan per thread (as the reference decoder handle). A plan owns
  * device scratch (decision arrays, the Fano work counter) that every decode reuses, so the decodes of
  * one plan must also be serialised on ONE stream; decodes on several streams need one plan each.
+ * After ccv_plan_reserve(max_blocks), ccv_decode_device of up to max_blocks blocks allocates and
+ * synchronises nothing (ccv_simulate_device: after one call of at least as many blocks), so either can
+ * be captured into a HIP graph and replayed -- the persistent kernels' group queue resets itself at
+ * the end of every launch (tests/test_gpu_graph.py).
  */
 #ifndef CCV_H
 #define CCV_H
