@@ -1107,3 +1107,47 @@ def test_device_channel_rejects_generic_codes(torch_cuda):
     plan = Plan(K9, SOFT, FLAG_GENERIC)
     with pytest.raises(Exception, match="register-trellis"):
         plan.simulate_device(1, 0, 10, 0.5)
+
+
+@pytest.mark.parametrize("channel", [SOFT, HARD], ids=["soft", "hard"])
+def test_group_queue_boundaries_one_plan(torch_cuda, channel):
+    """The K = 7 persistent kernels take their groups from the per-XCD queue (acs_persist.hpp
+    GroupQueue): every wave starts on one static group, then dequeues from eight heads over contiguous
+    eighths of the rest and steals from the other heads when its own is empty. Batch sizes around the
+    grid -- fewer groups than waves, exactly the grid, one group more, fewer extra groups than heads,
+    two grids less one, each with and without a ragged last group -- decoded back to back by ONE plan
+    (so every launch starts from the queue the previous one reset) equal the non-persistent kernel's
+    outputs, path metrics and fused error counts block for block."""
+    torch = torch_cuda
+    c = K7
+    plan = Plan(c, channel)
+    ref_plan = Plan(c, channel, FLAG_NO_PERSISTENT)
+    g = plan.persistent_waves()
+    assert g > 0
+    groups = [g // 2, g - 1, g, g + 1, g + 5, g + 8, 2 * g - 1, 2 * g + 9]
+    sizes = [64 * n + r for n in groups for r in (0, 37)]
+    nmax = max(sizes)
+    if channel == SOFT:
+        info, data = ch.awgn_blocks(c, nmax, ch.noise_scaling(2.5), 777)
+    else:
+        info, data = ch.bsc_blocks(c, nmax, 70000, 777)
+    d_in, d_info = _device(torch, data), _device(torch, info)
+    for nb in sizes:
+        res = []
+        for p in (plan, ref_plan):
+            d_out = torch.full((nb, c.out_bytes), 0xA5, dtype=torch.uint8, device="cuda")
+            d_pm = torch.full((nb,), -7, dtype=torch.int32, device="cuda")
+            d_err = torch.zeros(1, dtype=torch.int64, device="cuda")
+            p.decode_device(d_in, nb, d_out, d_path_metric=d_pm if channel == HARD else None,
+                            d_info=d_info, d_errors=d_err)
+            torch.cuda.synchronize()
+            res.append((d_out, d_pm, int(d_err.item())))
+        (out, pm, err), (out2, pm2, err2) = res
+        assert torch.equal(out, out2), (channel, nb)
+        assert err == err2, (channel, nb)
+        if channel == HARD:
+            assert torch.equal(pm, pm2), (channel, nb)
+    # the last (largest) batch against the oracle on a subsample
+    idx = np.arange(0, nmax, 97)
+    ref, ref_pm = _oracle(c, channel, data[idx])
+    assert np.array_equal(out.cpu().numpy()[idx], ref)
