@@ -166,15 +166,23 @@ constexpr bool twin_code() {
 // Output bytes (MSB-first, reference traceback :88) and the bit errors of the first blen bits
 // against the transmitted info bytes (consumer AWGN-channel/main.c:118-144). Static sizes: runtime
 // byte loops here cost the persistent kernels their register allocation (spills).
-template <int T, int BLEN>
-__device__ __forceinline__ uint32_t emit_block(const RegArgs& a, int b, uint64_t bits, uint64_t ref) {
+template <int T>
+__device__ __forceinline__ void store_block(const RegArgs& a, int b, uint64_t bits) {
   constexpr int OB = (T + 7) >> 3;
   uint8_t* o = a.out + (size_t)b * OB;
 #pragma unroll
   for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
+}
+template <int BLEN>
+__device__ __forceinline__ uint32_t block_errors(const RegArgs& a, uint64_t bits, uint64_t ref) {
   if (a.info == nullptr) return 0;
   constexpr uint64_t mask = BLEN >= 64 ? ~0ull : ~(~0ull >> BLEN);
   return (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
+}
+template <int T, int BLEN>
+__device__ __forceinline__ uint32_t emit_block(const RegArgs& a, int b, uint64_t bits, uint64_t ref) {
+  store_block<T>(a, b, bits);
+  return block_errors<BLEN>(a, bits, ref);
 }
 
 // The block's transmitted info bytes, MSB-aligned (bit 63 = info bit 0), or 0 without error counting.
@@ -371,7 +379,12 @@ __device__ __forceinline__ f32x4 lds_read_b128(uint32_t addr) {
 enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, kPersistCachedInput = 8,
              kPersistDepth2 = 16, kPersistNoMemRandom = 64, kPersistNoDma = 128, kPersistNoLdsRead = 256,
              kPersistInputNt = 512, kPersistQueue = 1024, kPersistStamp = 2048,
-             kPersistInfoFirst = 4096, kPersistQueueHop1 = 8192, kPersistQueueHop7 = 16384 };
+             kPersistInfoFirst = 4096, kPersistQueueHop1 = 8192, kPersistQueueHop7 = 16384,
+             kPersistDeferOut = 32768 };
+// kPersistDeferOut: a group's output stores (and the BSC path metric) are issued at the NEXT group's
+// start, behind its first DMA, instead of at the group's end: every vmcnt wait also waits for the
+// stores issued before it, and at the end of a group the next wait follows at once (the soft kernel's
+// chunk 0, the hard kernel's group start), so each group began with a store round trip.
 // Production schedules (round 6, tools/tail_bench.hip, profiles/r06c): the group queue with full
 // stealing -- soft 0.982x the static walk's time, hard 0.869x (+ the info loads ahead of the DMA, 0.997x
 // alone); 0, 1 or 7 steal hops measured alike.
@@ -379,12 +392,14 @@ enum : int { kPersistNoMem = 1, kPersistNoTraceback = 2, kPersistSelectAcs = 4, 
 // and its dequeue rate exceeds the heads' (code 0, K = 3, BSC: 40,625 groups in 0.104 ms = 390
 // dequeues/us; on the queue 0.104 -> 0.167 ms per launch, profiles/r06_bench) -- those keep the
 // static walk.
-constexpr int kPersistSoftProd = kPersistQueue | kPersistQueueHop7;
-constexpr int kPersistHardProd = kPersistQueue | kPersistQueueHop7 | kPersistInfoFirst;
+// Deferred output stores for every code (tools/defer_bench.hip, profiles/r06_defer: ABBA time ratio
+// 0.993 headline, 0.998 BSC K = 7, 0.995 code 0 BSC, 0.985 soft code 0; bit-identical).
+constexpr int kPersistSoftProd = kPersistQueue | kPersistQueueHop7 | kPersistDeferOut;
+constexpr int kPersistHardProd = kPersistQueue | kPersistQueueHop7 | kPersistInfoFirst | kPersistDeferOut;
 template <CodeSpec C>
-constexpr int persist_soft_opt() { return C.K >= 7 ? kPersistSoftProd : 0; }
+constexpr int persist_soft_opt() { return C.K >= 7 ? kPersistSoftProd : kPersistDeferOut; }
 template <CodeSpec C>
-constexpr int persist_hard_opt() { return C.K >= 7 ? kPersistHardProd : 0; }
+constexpr int persist_hard_opt() { return C.K >= 7 ? kPersistHardProd : kPersistDeferOut; }
 static_assert(kPersistQueue == 1024, "GroupWalk::QUEUE");
 // steal hops of the queue schedule (GroupQueue::resolve): 0, or the OPT bits above
 constexpr int queue_hops(int opt) {
@@ -485,6 +500,9 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
     if constexpr (DEPTH2) issue_chunk(g, 1, 1);
   }
   if (QUEUE && g < ngroups) ticket = Q.fetch(qx, lane);
+  constexpr bool DEFER = (ABLATE & kPersistDeferOut) != 0;
+  uint64_t pend_bits = 0;   // DEFER: the previous group's output, stored behind this group's first DMA
+  int pend_b = -1;
   for (int nxt = 0; g < ngroups; g = QUEUE ? nxt : g + stride_groups) {
     const int b = g * kRegThreads + lane;
     const bool has_next = g + stride_groups < ngroups;
@@ -557,6 +575,10 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
         } else {
           issue_chunk(has_next ? g + stride_groups : g, c + 2 - NCH, c % 2);
         }
+        if constexpr (DEFER && c == 0) {
+          asm volatile("" ::: "memory");   // behind the DMA: the next chunk's wait finds them done
+          if (pend_b >= 0) store_block<T>(a, pend_b, pend_bits);
+        }
       }
       auto step_at = [&]<int u>() __attribute__((always_inline)) {
         constexpr int t = c * PF + u;
@@ -592,17 +614,17 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
 #pragma unroll
       for (int k = 0; k < IB; ++k) ref |= (uint64_t)info[k] << (56 - 8 * k);
       // lanes past the batch store nothing (exec-masked)
-      if (b < nb) {
-        uint8_t* o = a.out + (size_t)b * OB;
-#pragma unroll
-        for (int k = 0; k < OB; ++k) o[k] = (uint8_t)(bits >> (56 - 8 * k));
-        if (a.info != nullptr) {
-          constexpr uint64_t mask = BLEN >= 64 ? ~0ull : ~(~0ull >> BLEN);
-          errors += (uint32_t)__builtin_popcountll((bits ^ ref) & mask);
-        }
+      if constexpr (DEFER) {
+        if (b < nb) errors += block_errors<BLEN>(a, bits, ref);
+        pend_b = b < nb ? b : -1;
+        pend_bits = bits;
+      } else if (b < nb) {
+        store_block<T>(a, b, bits);
+        errors += block_errors<BLEN>(a, bits, ref);
       }
     }
   }
+  if (DEFER && pend_b >= 0) store_block<T>(a, pend_b, pend_bits);
   // the last group's look-ahead DMAs write LDS: they must land before the workgroup (and its LDS
   // allocation) ends
   wait_vmcnt<0>();
@@ -696,6 +718,10 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
   int buf = 0;
   if (g < ngroups) issue_group(g, 0);
   if (QUEUE && g < ngroups) ticket = Q.fetch(qx, lane);
+  constexpr bool DEFER = (OPT & kPersistDeferOut) != 0;
+  uint64_t pend_bits = 0;   // DEFER: the previous group's output and path metric
+  uint32_t pend_pm = 0;
+  int pend_b = -1;
   for (int nxt = 0; g < ngroups; g = QUEUE ? nxt : g + stride_groups, buf ^= 1) {
     const int b = g * kRegThreads + lane;
     ++ndone;
@@ -718,6 +744,13 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
       }
     } else if (g + stride_groups < ngroups) {
       issue_group(g + stride_groups, buf ^ 1);
+    }
+    if constexpr (DEFER) {   // behind the next group's DMA: the next group start finds them done
+      asm volatile("" ::: "memory");
+      if (pend_b >= 0) {
+        if (a.path_metric) a.path_metric[pend_b] = (int32_t)pend_pm;
+        store_block<T>(a, pend_b, pend_bits);
+      }
     }
     const uint32_t row_addr = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * kBuf + lane * T);
     if constexpr ((OPT & kPersistInfoFirst) == 0) info = load_info<BLEN>(a, b);
@@ -794,9 +827,20 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
       }
       st = (uint32_t)argmin_state<S, uint32_t>(Mu, 0xFF00u, best);
     }
-    if (a.path_metric) a.path_metric[b] = (int32_t)best;
     const uint64_t bits = traceback_regs<C.K, DW, BLEN>(D, st, a.blen);
-    errors += emit_block<T, BLEN>(a, b, bits, info);
+    if constexpr (DEFER) {
+      errors += block_errors<BLEN>(a, bits, info);
+      pend_b = b;
+      pend_bits = bits;
+      pend_pm = best;
+    } else {
+      if (a.path_metric) a.path_metric[b] = (int32_t)best;
+      errors += emit_block<T, BLEN>(a, b, bits, info);
+    }
+  }
+  if (DEFER && pend_b >= 0) {
+    if (a.path_metric) a.path_metric[pend_b] = (int32_t)pend_pm;
+    store_block<T>(a, pend_b, pend_bits);
   }
   if constexpr (QUEUE) Q.exit(lane);
   accumulate_errors(a, errors);
