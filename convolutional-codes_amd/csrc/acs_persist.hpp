@@ -673,6 +673,8 @@ void viterbi_hard_persist(RegArgs a, int ngroups) {
   using DW = DecWord<S>;
   const int lane = threadIdx.x;
   const int stride_groups = gridDim.x;
+  // sized for T = 64 (buffers sized by T, whole 1 KiB DMA instructions, give code 0 six waves per
+  // SIMD instead of five: 1.019x the time, tools/defer_bench.hip round 6, profiles/r06_defer)
   constexpr int kBuf = kRegThreads * kHardPersistMaxT;
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kBuf];
   const unsigned char* in = reinterpret_cast<const unsigned char*>(a.in);

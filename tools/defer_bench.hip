@@ -142,7 +142,7 @@ int main() {
       CHECK(hipMemcpy(pa.data(), d_pm_a, (size_t)n * 4, hipMemcpyDeviceToHost));
       CHECK(hipMemcpy(pb.data(), d_pm_b, (size_t)n * 4, hipMemcpyDeviceToHost));
       const bool same = p == q && (!c.hard || pa == pb);
-      printf("%s, %d blocks: deferred outputs%s %s\n", c.name, n, c.hard ? " and path metrics" : "",
+      printf("%s, %d blocks: variant outputs%s %s\n", c.name, n, c.hard ? " and path metrics" : "",
              same ? "identical" : "DIFFER");
       bad += !same;
     }
@@ -158,7 +158,7 @@ int main() {
       bt += b0 + b1;
     }
     const double bits = (double)nb * 40;
-    printf("%-32s production %.4f ms (%.1f Gbit/s)  deferred stores %.4f ms (%.1f Gbit/s)  time ratio %.3f\n",
+    printf("%-32s A %.4f ms (%.1f Gbit/s)  B (variant) %.4f ms (%.1f Gbit/s)  time ratio %.3f\n",
            c.name, at / 8, bits / (at / 8 * 1e-3) / 1e9, bt / 8, bits / (bt / 8 * 1e-3) / 1e9, r / 4);
     fflush(stdout);
   }
