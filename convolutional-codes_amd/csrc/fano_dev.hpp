@@ -154,7 +154,8 @@ __host__ __device__ constexpr size_t fano_node_bytes(int T, size_t metric_bytes)
 //   kRowsGlobal: each pass first issues the loads of the two rows a move can land on (cur - 1,
 //     cur + 1) and the lane keeps its own node's row in registers, so the load latency overlaps the
 //     pass instead of following it (hard input or rate 1/2: a row is a byte or a float4).
-//   kRowsLds: as kRowsGlobal, the block's rows copied into LDS when the lane takes the block.
+//   kRowsLds: as kRowsGlobal, the block's rows copied into LDS when the lane takes the block; the two
+//     rows are read as soon as the previous pass has decided its move (round 6).
 // (Round 5 measured and removed a register window of rows cur - 1, cur, cur + 1 with one load per
 // move issued a pass ahead: 67 -> 48 Mbit/s soft, 222 -> 156 BSC, profiles/r05b/.)
 //   kRowsIQ / kRowsIQLds (round 6, soft rate 1/2, option "fano_input" 1): the rows are the received
@@ -311,6 +312,18 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
   bool inback = false, moved = false;
   uint32_t moves = 0, spass = 0;
   Row row0{};   // received row of node cur
+  // the rows of nodes cur - 1 and cur + 1, where this pass's move can land. Rows in LDS: read as soon
+  // as the previous pass has decided its move, so their latency overlaps the rest of that pass too
+  // (round 6, BSC 212 -> 232 Mbit/s); rows in global memory: at the top of the pass (the early form
+  // measured 1-1.6 % slower there, profiles/r06_fano_early/)
+  constexpr bool EARLY = LDSROWS;
+  Row rowm{}, rowp{};
+  auto prefetch_rows = [&](int c) {
+    if constexpr (ROWS && EARLY) {
+      rowm = row_at(c > 0 ? c - 1 : 0);
+      rowp = row_at(c + 1 < T ? c + 1 : T - 1);
+    }
+  };
   auto as_bits = [](MT v) -> uint32_t {
     if constexpr (HARD) return (uint32_t)v;
     else return __float_as_uint(v);
@@ -386,6 +399,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     moves = h[11];
     spass = 0;
     if constexpr (ROWS) row0 = row_at(cur);
+    prefetch_rows(cur);
   };
   // start a search (:108-124 reset, then the root's branch metrics)
   auto start = [&]() {
@@ -398,6 +412,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     load_rows();
     spass = 0;
     if constexpr (ROWS) row0 = row_at(0);
+    prefetch_rows(0);
     metric[lane] = (MT)0;
     cur = 0;
     frontier = 0;
@@ -462,8 +477,7 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
     const MT mprev = metric[cm * kFanoThreads + lane];
     const uint32_t fprev = flag_get(cm);
     const uint32_t fold = flag_get(cur >= K ? cur - K : 0);
-    Row rowm{}, rowp{};
-    if constexpr (ROWS) {
+    if constexpr (ROWS && !EARLY) {
       rowm = row_at(cm);
       rowp = row_at(cur + 1 < T ? cur + 1 : T - 1);
     }
@@ -507,11 +521,20 @@ __global__ __launch_bounds__(kFanoThreads) void fano_decode(FanoArgs a) {
       start();
       continue;
     }
+    Row nextm{}, nextp{};   // the next pass's candidate rows, issued right away (EARLY)
+    if constexpr (ROWS && EARLY) {
+      nextm = row_at(ncur > 0 ? ncur - 1 : 0);
+      nextp = row_at(ncur + 1 < T ? ncur + 1 : T - 1);
+    }
     metric[(fwd ? ncur : T) * kFanoThreads + lane] = ms;
     if constexpr (ROWS) row0.pick(fwd, rowp, bstep, rowm);
     MT n0, n1;
     uint32_t sw;
     node_metrics(rx, ncur, st, row0, n0, n1, sw);
+    if constexpr (ROWS && EARLY) {
+      rowm = nextm;
+      rowp = nextp;
+    }
     tm0 = need ? n0 : tm0;
     tm1 = need ? n1 : tm1;
     dec = fwd ? sw : dec;
