@@ -1,0 +1,16 @@
+#!/bin/bash
+# A/B of a stack-decoder kernel change on one box: GPU tests of the new build, then bench.py soft and
+# BSC (16 frames, config 5), round-robin against a copy of the previous core library
+# (lib/libccv_core_r6base.so, loaded through CCV_CORE_LIB). Logs in gpurun_out/sab/.
+set -u
+mkdir -p gpurun_out/sab
+timeout -k 10 400 python -u -m pytest tests/test_gpu_stack.py tests/test_gpu_seq_fuzz.py -q --timeout 200 --timeout-method thread -m gpu > gpurun_out/sab/pytest.log 2>&1 || { tail -20 gpurun_out/sab/pytest.log; exit 1; }
+tail -2 gpurun_out/sab/pytest.log
+for rep in 1 2 3; do
+  for v in base new; do
+    if [ $v = base ]; then export CCV_CORE_LIB=libccv_core_r6base.so; else unset CCV_CORE_LIB; fi
+    timeout -k 10 200 python bench.py --decoder stack --frames 16 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/sab/soft_${v}_${rep}.log 2>&1 || exit 1
+    timeout -k 10 200 python bench.py --decoder stack --channel bsc --frames 16 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/sab/bsc_${v}_${rep}.log 2>&1 || exit 1
+    echo "$v $rep soft $(grep -o '"value": [0-9.]*' gpurun_out/sab/soft_${v}_${rep}.log | head -1) bsc $(grep -o '"value": [0-9.]*' gpurun_out/sab/bsc_${v}_${rep}.log | head -1)"
+  done
+done
