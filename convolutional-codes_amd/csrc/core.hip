@@ -892,12 +892,16 @@ int ccv_fano_decode_device(ccv_plan* p, const void* d_in, size_t nblocks, uint8_
   a.info = d_info;
   a.err = d_info ? d_errors : nullptr;
   a.iterations = d_iterations;
-  // two-pass schedule (fano_dev.hpp): park searches after 4000 x T moves (0.4 of the timeout), resume
-  // them in pass 2; option "fano_cap" overrides, 0 = one pass. Measured caps (tools/fano_caps.py,
-  // profiles/r03_fano_caps.txt; K=15, 104 frames): 4 dB 47.3 (one pass) -> 49.4 Mbit/s at 216,000
-  // moves, but 41.5 at 20,000-108,000 (half the searches park and the parking costs more than the
-  // tail it saves); 6 dB 153 -> 165 at 108,000; BSC 222 -> 239 at 54,000.
-  long cap = p->opt.fano_cap >= 0 ? (long)p->opt.fano_cap : 4000L * a.T;
+  // two-pass schedule (fano_dev.hpp): park searches after 6000 x T moves (soft, 0.6 of the timeout)
+  // or 1000 x T (hard), resume them in pass 2; option "fano_cap" overrides, 0 = one pass. Measured
+  // caps (K = 15, 104 frames): round 3 (tools/fano_caps.py, profiles/r03_fano_caps.txt) 4 dB 47.3 (one
+  // pass) -> 49.4 Mbit/s at 216,000 moves, 41.5 at 20,000-108,000 (half the searches park and the
+  // parking costs more than the tail it saves); round 6 on the current kernels (tools/fano_cap_sweep.sh,
+  // profiles/r06_fano_cap/; mean of 2-4 round-robin runs): soft 4 dB 51.6 / 67.4 / 68.3 / 68.4 / 66.6
+  // / 64.9 at 108,000 / 216,000 / 270,000 / 324,000 / 378,000 / 432,000 (61.1 one pass); BSC 5 %
+  // 230.1 / 239.9 / 236.9 at 216,000 / 54,000 / one pass.
+  long cap = p->opt.fano_cap >= 0 ? (long)p->opt.fano_cap
+                                  : (p->d.channel == CCV_HARD ? 1000L : 6000L) * a.T;
   if (cap > 0 && nblocks > 64) {
     const size_t cap_slots = nblocks / 8 > 65536 ? nblocks / 8 : (nblocks < 65536 ? nblocks : 65536);
     const size_t mt = p->d.channel == CCV_HARD ? sizeof(int32_t) : sizeof(float);

@@ -210,7 +210,8 @@ int ccv_decode_host(ccv_plan* plan, const void* in, size_t nblocks, uint8_t* out
  *                                    1 LDS, 2 both candidates prefetched
  *                 "fano_symtab"      -1 auto (table for hard input), 0, 1
  *                 "fano_order"       1 noisiest blocks first for soft input (default), 0 natural order
- *                 "fano_cap"         -1 default (4000 x T moves), 0 one pass, else moves before parking
+ *                 "fano_cap"         -1 default (6000 x T moves soft, 1000 x T hard), 0 one pass, else moves
+ *                                    before parking
  *                 "fano_count_moves" 1: d_iterations gets moves instead of timeout ticks (diagnostics)
  *                 "fano_input"       0 the demapper's distances (default: the reference decoder's input),
  *                                    1 received points float [nb][T][2] (CCV_CHANNEL_IQ frames; soft,
