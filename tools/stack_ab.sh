@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of a stack-decoder kernel change on one box: GPU tests of the new build, then bench.py soft and
 # BSC (16 frames, config 5), round-robin against a copy of the previous core library
-# (lib/libccv_core_r6base.so, loaded through CCV_CORE_LIB). Logs in gpurun_out/sab/.
+# (lib/libccv_core_r6base.so, loaded through CCV_CORE_LIB: copy lib/libccv_core.so there before
+# rebuilding with the change, delete it afterwards -- lib/ travels with every gpurun call). Logs in gpurun_out/sab/.
 set -u
 mkdir -p gpurun_out/sab
 timeout -k 10 400 python -u -m pytest tests/test_gpu_stack.py tests/test_gpu_seq_fuzz.py -q --timeout 200 --timeout-method thread -m gpu > gpurun_out/sab/pytest.log 2>&1 || { tail -20 gpurun_out/sab/pytest.log; exit 1; }
