@@ -424,7 +424,7 @@ void viterbi_soft_persist(RegArgs a, int ngroups) {
   constexpr int G = C.K - 1;                  // growth steps
   constexpr int T = BLEN + G;                 // trellis steps per block
   constexpr int NCH = (T + PF - 1) / PF;
-  constexpr int IB = (BLEN + 7) >> 3, OB = (T + 7) >> 3;
+  constexpr int IB = (BLEN + 7) >> 3;
   static_assert(BLEN >= 1 && BLEN <= kPersistMaxMain, "decisions of the main steps live in VGPRs");
   static_assert(NCH >= 4 && NCH % 2 == 0, "buffer = chunk parity across groups");
   constexpr bool DEPTH2 = (ABLATE & kPersistDepth2) != 0;   // two chunks in flight
